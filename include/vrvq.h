@@ -1,0 +1,172 @@
+/*
+ * vrvq.h — C-ABI of the MI355X (gfx950) VRVQ hot path: encode -> residual VQ -> decode.
+ *
+ * The reference (lixinghe1999/VRVQ) has no FFI layer: its operator surface is the Python
+ * module API of models/layers.py, models/quantize.py, models/utils.py and
+ * models/dac_vrvq.py. Every entry point below replaces one reference operator (cited
+ * file:line) and is bound from Python by ctypes in vrvq_amd/_lib.py (INTEGRATION.md shows
+ * the binding a maintainer would add on the reference side).
+ *
+ * Conventions
+ *   - All tensors are contiguous, row-major, in device (HBM) memory; fp32 unless noted.
+ *   - The caller owns every buffer (inputs, outputs, workspaces); nothing is allocated here.
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = legacy default stream)
+ *     and graph-capturable (no allocation, no host sync inside).
+ *   - Return value: 0 on success, otherwise a vrvq_status_t (argument errors, detected
+ *     on the host before any launch) or the hipError_t of the failed launch.
+ *     vrvq_status_string() turns either into text.
+ */
+#ifndef VRVQ_H_
+#define VRVQ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vrvq_stream_t; /* hipStream_t */
+
+enum vrvq_status_t {
+  VRVQ_OK = 0,
+  VRVQ_ERR_ARG = 10001,      /* null pointer / non-positive size / unsupported shape */
+  VRVQ_ERR_UNSUPPORTED = 10002 /* shape outside the instantiated kernel set */
+};
+
+/* Conv epilogue selector (vrvq_conv1d.epilogue). */
+enum vrvq_epilogue_t { VRVQ_EPI_NONE = 0, VRVQ_EPI_TANH = 1, VRVQ_EPI_SIGMOID = 2 };
+
+const char* vrvq_status_string(int status);
+/* Library version (major*10000 + minor*100 + patch). */
+int vrvq_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Weight preparation (once per load_state_dict; the reference recomputes weight norm on
+ * every forward via the torch.nn.utils.weight_norm pre-hook).
+ * ------------------------------------------------------------------------------------- */
+
+/* w[r, :] = v[r, :] * (g[r] / ||v[r, :]||_2), r < rows, row length = cols.
+ * Replaces torch.nn.utils.weight_norm(dim=0) as used by WNConv1d / WNConvTranspose1d
+ * (models/layers.py:17-22). For Conv1d rows = Cout, cols = Cin*k; for ConvTranspose1d
+ * rows = Cin, cols = Cout*k (weight-norm dim 0 is in_channels there). */
+int vrvq_weight_norm(const float* g, const float* v, int rows, int cols, float* w,
+                     vrvq_stream_t stream);
+
+/* inv[c] = 1 / (alpha[c] + 1e-9f). Snake's reciprocal, models/layers.py:30. */
+int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv, vrvq_stream_t stream);
+
+/* Codebook normalisation for VectorQuantize.decode_latents (models/quantize.py:92-99):
+ * cbn[n,:] = cb[n,:] / max(||cb[n,:]||, 1e-12); c2[n] = sum_k cbn[n,k]^2.
+ * cb is [rows][dim] (rows = nq * codebook_size for a stacked RVQ). */
+int vrvq_codebook_prep(const float* cb, int rows, int dim, float* cbn, float* c2,
+                       vrvq_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Snake-fused 1-D convolution (implicit GEMM on v_mfma_f32_32x32x2_f32).
+ *
+ *   y[b,co,t] = epi( residual[b,co,t] + (bias[co] + sum_{ci,k} W[co,ci,k] *
+ *                    snake_ci(x[b,ci, t*stride - pad + k*dil])) )
+ *   snake_c(v) = v + inv_alpha[c] * sin(alpha[c]*v)^2     (skipped when alpha == NULL)
+ *
+ * Replaces Snake1d -> WNConv1d (models/layers.py:26-41, 17-18) and the ResidualUnit skip
+ * (models/layers.py:63-68), EncoderBlock / Encoder / Decoder convs
+ * (models/layers.py:71-89, models/dac_vrvq.py:19-80), the ImportanceSubnet convs + Sigmoid
+ * (models/importance_subnet.py:38-45) and the decoder Tanh (models/dac_vrvq.py:74).
+ *
+ * w_packed: [Cin][k][cout_pad] (cout_pad >= Cout, multiple of 128, zero padded) as produced
+ * by vrvq_pack_conv1d_weight. residual (nullable) has the output's shape.
+ * tout must equal floor((tin + 2*pad - dil*(k-1) - 1)/stride) + 1.
+ * ------------------------------------------------------------------------------------- */
+int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
+                const float* inv_alpha, const float* w_packed, int cout, int cout_pad, int k,
+                int stride, int pad, int dil, const float* bias, const float* residual,
+                int epilogue, float* y, int tout, vrvq_stream_t stream);
+
+/* Pack a folded Conv1d weight w[Cout][Cin][k] into [Cin][k][cout_pad]. */
+int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
+                            float* w_packed, vrvq_stream_t stream);
+
+/* Snake-fused ConvTranspose1d, kernel = 2*stride, padding = stride/2 (even stride), i.e.
+ * the DecoderBlock upsampler (models/layers.py:92-103): y has length tin*stride.
+ * Computed as a polyphase 2-tap conv with cout*stride phase-channels:
+ *   y[b,co,m*s+r-p] = bias[co] + sum_ci W[ci,co,r]*xs[ci,m] + W[ci,co,r+s]*xs[ci,m-1].
+ * w_packed from vrvq_pack_convt1d_weight ([Cin][2][cout*stride padded to 128]). */
+int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin, const float* alpha,
+                          const float* inv_alpha, const float* w_packed, int cout,
+                          int cout_pad, int stride, const float* bias, float* y,
+                          vrvq_stream_t stream);
+
+/* Pack a folded ConvTranspose1d weight w[Cin][Cout][2*stride] into the polyphase layout. */
+int vrvq_pack_convt1d_weight(const float* w, int cin, int cout, int stride, int cout_pad,
+                             float* w_packed, vrvq_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Residual vector quantisation (VBRResidualVectorQuantize.forward, models/quantize.py:328-443;
+ * per stage VectorQuantize.forward/decode_latents, models/quantize.py:42-103).
+ *
+ * Stage 1 (vrvq_rvq_codes): the sequential residual chain, all nq stages in one launch.
+ * Per frame (b,t) and stage i:
+ *   z_e   = W_in[i] r + b_in[i]                    (in_proj, WN k=1 conv D->d)
+ *   e     = z_e / max(||z_e||, 1e-12)
+ *   idx   = argmin_n ( (sum e^2 - 2 e.cbn[i,n]) + c2[i,n] ), lowest n on ties
+ *   zq    = cb[i, idx]                             (raw codebook row)
+ *   loss  = mean_k (z_e - zq)^2                    (commitment == codebook loss in forward)
+ *   zst   = z_e + (zq - z_e)                       (straight-through value)
+ *   r    -= W_out[i] zst + b_out[i]                (out_proj, WN k=1 conv d->D)
+ *
+ *   z       [B][D][T]         encoder output
+ *   w_in_t  [nq][D][d]        folded in_proj weight, transposed (d fastest)
+ *   b_in    [nq][d]
+ *   cb, cbn [nq][N][d]        raw / normalised codebooks; c2 [nq][N]
+ *   w_out   [nq][D][d]        folded out_proj weight; b_out [nq][D]
+ * outputs:
+ *   codes   [B][nq][T] int64  (torch argmax indices)
+ *   latents [B][nq*d][T]      concatenated z_e
+ *   loss_pf [B][nq][T]        per-frame loss
+ *   zst     [B][nq][T][d]     straight-through codebook vectors (input of stage 2)
+ * Supported: D == 1024 (latent_dim of every shipped config), d == 8, N % 256 == 0.
+ * ------------------------------------------------------------------------------------- */
+int vrvq_rvq_codes(const float* z, int batch, int dim, int frames, int nq, int ncode,
+                   int cdim, const float* w_in_t, const float* b_in, const float* cb,
+                   const float* cbn, const float* c2, const float* w_out, const float* b_out,
+                   int64_t* codes, float* latents, float* loss_pf, float* zst,
+                   vrvq_stream_t stream);
+
+/* Stage 2 (vrvq_rvq_expand): HBM-streaming expansion + importance gating.
+ *   z_q_is[b,i,:,t] = W_out[i] zst[b,i,t] + b_out[i]          (bit-identical to stage 1)
+ *   s[b,t]          = (imp[b,t] * level) * nq                 (models/quantize.py:389)
+ *   mask[b,i,t]     = s[b,t] - i >= 0 ? 1 : 0                 (models/utils.py:45-61)
+ *   z_q[b,:,t]      = sum_i mask[b,i,t] * z_q_is[b,i,:,t]     (models/quantize.py:420-421)
+ * imp == NULL selects the reference's CBR branch (mask = 1, models/quantize.py:397-400).
+ * z_q_is may be NULL (not materialised). mask may be NULL. */
+int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames, int nq, int cdim,
+                    const float* w_out, const float* b_out, const float* imp, float level,
+                    float* z_q_is, float* z_q, float* mask, vrvq_stream_t stream);
+
+/* Masked loss reduction (models/quantize.py:422-423): out[0] = (loss_pf*mask).sum(1).mean().
+ * One workgroup, fixed order (deterministic). */
+int vrvq_masked_loss(const float* loss_pf, const float* mask, int batch, int nq, int frames,
+                     float* out, vrvq_stream_t stream);
+
+/* generate_mask_hard (models/utils.py:55-61): mask[b,n,t] = (s[b,t] - n >= 0). s is [B][T]. */
+int vrvq_mask_hard(const float* s, int batch, int frames, int nq, float* mask,
+                   vrvq_stream_t stream);
+
+/* Scaled importance map: s[b,t] = (imp[b,t] * a) * c (two separate fp32 roundings, matching
+ * `imp_map * level * n_codebooks` at models/quantize.py:389 with a=level, c=nq, and
+ * `imp_map * (level*n_q)` at scripts/inference.py:96-97 with a=level*n_q, c=1). */
+int vrvq_scale_imp(const float* imp, int n, float a, float c, float* s, vrvq_stream_t stream);
+
+/* Masked sum over codebooks (scripts/inference.py:99-100):
+ * z_q[b,:,t] = sum_i mask[b,i,t] * z_q_is[b,i,:,t]. */
+int vrvq_masked_sum(const float* z_q_is, const float* mask, int batch, int nq, int dim,
+                    int frames, float* z_q, vrvq_stream_t stream);
+
+/* cal_bpf_from_mask (models/utils.py:64-73): out[0] = sum(mask*bits[n]) / (B*T). */
+int vrvq_bpf(const float* mask, const float* bits, int batch, int nq, int frames, float* out,
+             vrvq_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VRVQ_H_ */

@@ -1,0 +1,235 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE PyTorch CPU path.
+
+Run in the build container only (the reference is not shipped to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--ref /root/reference]
+
+The reference (lixinghe1999/VRVQ) is imported from its source tree with stub modules for the
+three third-party packages that are absent here and that the hot path does not use
+arithmetically: `audiotools` (only `ml.BaseModel`, an nn.Module base with a
+`device` property, and the `AudioSignal` name), `torchmetrics` (imported, unused on the path)
+and nothing else. Weights come from vrvq_amd.recipe (name-seeded PCG64), so the GPU tests can
+regenerate identical weights without a checkpoint. Outputs are .npz fixtures (inputs and
+expected outputs: data only) plus a JSON manifest.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import types
+from collections import namedtuple
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from vrvq_amd.recipe import recipe_state_dict, shapes_of, synthetic_audio  # noqa: E402
+
+LEVELS = [0.25, 0.5, 1.0, 2.0]
+MASK_KAT_S = [0.0, 1.0, 2.0, 7.0, 8.0, -0.5, 3.9999999, 4.5, 27.0, 31.9999]
+
+
+def install_stubs():
+    at = types.ModuleType("audiotools")
+    ml = types.ModuleType("audiotools.ml")
+
+    class BaseModel(torch.nn.Module):
+        @property
+        def device(self):
+            return next(self.parameters()).device
+
+    ml.BaseModel = BaseModel
+    at.ml = ml
+    at.AudioSignal = type("AudioSignal", (), {})
+    at.STFTParams = namedtuple("STFTParams", ["window_length", "hop_length", "window_type",
+                                              "match_stride", "padding_type"])
+    sys.modules["audiotools"] = at
+    sys.modules["audiotools.ml"] = ml
+    sys.modules["torchmetrics"] = types.ModuleType("torchmetrics")
+
+
+def load_ref(ref_root):
+    install_stubs()
+    sys.path.insert(0, ref_root)
+    from models.dac_vrvq import DAC_VRVQ  # noqa: E402
+    from models import utils as ref_utils  # noqa: E402
+    return DAC_VRVQ, ref_utils
+
+
+def yml_kwargs(ref_root, rel):
+    sys.path.insert(0, REPO)
+    from vrvq_amd.config import load_config, model_kwargs
+    cwd = os.getcwd()
+    os.chdir(ref_root)  # argbind resolves $include relative to the working directory
+    try:
+        return model_kwargs(load_config(os.path.join(ref_root, rel)))
+    finally:
+        os.chdir(cwd)
+
+
+def build(DAC, kw, seed=0):
+    torch.manual_seed(0)
+    m = DAC(**kw)
+    sd = m.state_dict()
+    rec = recipe_state_dict(shapes_of(sd), seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in rec.items()}, strict=True)
+    m.eval()
+    return m
+
+
+def top2_gap(z_e_list, quantizers):
+    """Min (second - best) distance over frames, per stage (argmin stability diagnostic)."""
+    gaps = []
+    for ze, q in zip(z_e_list, quantizers):
+        enc = torch.nn.functional.normalize(ze.permute(0, 2, 1).reshape(-1, ze.shape[1]))
+        cb = torch.nn.functional.normalize(q.codebook.weight)
+        dist = enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cb.t() + cb.pow(2).sum(1, keepdim=True).t()
+        s = torch.sort(dist, dim=1).values
+        gaps.append(float((s[:, 1] - s[:, 0]).min()))
+    return gaps
+
+
+def sweep(model, ref_utils, x_pad, enc, n_q):
+    """scripts/inference.py:95-112 without SI-SDR / file output."""
+    out = {}
+    imp_map = enc["imp_map"]
+    for li, level in enumerate(LEVELS):
+        level_scaled = level * n_q
+        imp_scaled = imp_map * level_scaled
+        mask = ref_utils.generate_mask_hard(imp_scaled, nq=n_q)
+        z_q = torch.sum(enc["z_q_is"] * mask[:, :, None, :], dim=1, keepdim=False)
+        with torch.no_grad():
+            recon = model.decode(z_q)
+        bpf = ref_utils.cal_bpf_from_mask(mask, bits_per_codebook=[10] * n_q)
+        kbps = bpf * np.floor(model.sample_rate / model.hop_length) / 1000
+        out[f"sweep{li}_mask"] = mask.numpy()
+        out[f"sweep{li}_zq_norm"] = z_q.norm(dim=1).numpy()
+        out[f"sweep{li}_recon_s8"] = recon[..., ::8].numpy()
+        out[f"sweep{li}_bpf"] = np.float64(bpf)
+        out[f"sweep{li}_kbps"] = np.float64(kbps)
+        s = imp_scaled.numpy().astype(np.float64)
+        out[f"sweep{li}_tie_margin"] = np.float64(np.min(np.abs(s - np.round(s))))
+    return out
+
+
+def model_fixture(DAC, ref_utils, kw, batch, name, manifest, n_quantizers=None, full_z=True):
+    model = build(DAC, kw)
+    audio = synthetic_audio(batch, 44100, seed=1234)
+    x = torch.from_numpy(audio)
+    res = {"audio_in": audio}
+    with torch.no_grad():
+        xp = model.preprocess(x, 44100)
+        z, feat = model.encoder(xp, return_feat=True)
+        if model.model_type == "VBR":
+            enc = model.quantizer(z, n_quantizers, feat, 1)
+        else:
+            enc = model.quantizer(z, n_quantizers)
+        fwd = model(x, 44100, n_quantizers, 1) if model.model_type == "VBR" else model(x, 44100, n_quantizers)
+        # per-stage latents for the argmin-gap diagnostic
+        nlat = enc["latents"].shape[1] // 8
+        ze_list = [enc["latents"][:, 8 * i: 8 * i + 8] for i in range(nlat)]
+        gaps = top2_gap(ze_list, model.quantizer.quantizers)
+    if full_z:
+        res["z"] = z.numpy()
+        res["feat"] = feat.numpy()
+    res["codes"] = enc["codes"].numpy()
+    res["latents"] = enc["latents"].numpy()
+    res["z_q"] = enc["z_q"].numpy()
+    res["commitment_loss"] = np.float32(enc["commitment_loss"].item())
+    res["codebook_loss"] = np.float32(enc["codebook_loss"].item())
+    if enc.get("imp_map") is not None:
+        res["imp_map"] = enc["imp_map"].numpy()
+    if enc.get("mask_imp") is not None:
+        res["mask_imp"] = enc["mask_imp"].numpy()
+    if enc.get("z_q_is") is not None:
+        zqis = enc["z_q_is"]
+        res["z_q_is_norm"] = zqis.norm(dim=(2, 3)).numpy()
+        res["z_q_is_s16"] = zqis[:, :, ::16, :].numpy()
+    res["audio_out"] = fwd["audio"].numpy()
+    if model.model_type == "VBR" and n_quantizers is None:
+        res.update(sweep(model, ref_utils, xp, enc, model.n_codebooks))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+    imp = enc.get("imp_map")
+    manifest[name] = {
+        "kwargs": kw, "batch": batch, "length": 44100, "audio_seed": 1234, "weight_seed": 0,
+        "n_quantizers": n_quantizers, "delay": int(model.delay),
+        "min_top2_gap_per_stage": gaps,
+        "imp_range": [float(imp.min()), float(imp.max())] if imp is not None else None,
+        "n_params": int(sum(p.numel() for p in model.parameters())),
+        "state_dict": {k: list(v.shape) for k, v in model.state_dict().items()},
+    }
+    print(name, "gap", min(gaps), "imp", manifest[name]["imp_range"], "delay", model.delay)
+    return model
+
+
+def rvq_stress_fixture(DAC, kw, name, manifest, batch=4, frames=50, seed=7):
+    """RVQ unit at random latents (many frames): z, feat -> quantizer outputs."""
+    model = build(DAC, kw)
+    g = torch.Generator().manual_seed(seed)
+    z = torch.randn(batch, model.latent_dim, frames, generator=g) * 0.5
+    feat = torch.randn(batch, model.latent_dim, frames, generator=g) * 0.5
+    with torch.no_grad():
+        enc = model.quantizer(z, None, feat, 1)
+        nlat = enc["latents"].shape[1] // 8
+        gaps = top2_gap([enc["latents"][:, 8 * i: 8 * i + 8] for i in range(nlat)],
+                        model.quantizer.quantizers)
+    res = {"z": z.numpy(), "feat": feat.numpy(), "codes": enc["codes"].numpy(),
+           "latents": enc["latents"].numpy(), "z_q": enc["z_q"].numpy(),
+           "imp_map": enc["imp_map"].numpy(), "mask_imp": enc["mask_imp"].numpy(),
+           "commitment_loss": np.float32(enc["commitment_loss"].item()),
+           "z_q_is_norm": enc["z_q_is"].norm(dim=(2, 3)).numpy()}
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+    manifest[name] = {"kwargs": kw, "batch": batch, "frames": frames, "z_seed": seed,
+                      "weight_seed": 0, "min_top2_gap_per_stage": gaps,
+                      "state_dict": {k: list(v.shape) for k, v in model.state_dict().items()}}
+    print(name, "gap", min(gaps))
+
+
+def mask_kat(ref_utils, manifest):
+    s = torch.tensor(MASK_KAT_S, dtype=torch.float32).reshape(1, 1, -1)
+    out = {}
+    for nq in (8, 28, 32):
+        m = ref_utils.generate_mask_hard(s, nq)
+        out[str(nq)] = {"mask": m[0].tolist(), "bpf10": ref_utils.cal_bpf_from_mask(m, [10] * nq)}
+    ste = ref_utils.generate_mask_ste(s.clone(), 8, alpha=2.0)
+    out["ste8_alpha2"] = ste[0].tolist()
+    manifest["mask_kat"] = {"s": [float(v) for v in s.reshape(-1)], "results": out}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default=os.environ.get("VRVQ_REFERENCE", "/root/reference"))
+    args = ap.parse_args()
+    torch.set_num_threads(os.cpu_count() or 8)
+    DAC, ref_utils = load_ref(args.ref)
+    manifest = {"generator": "tests/golden/make_golden.py", "torch": torch.__version__,
+                "reference": "lixinghe1999/VRVQ @ 2025-07-25 (/root/reference)",
+                "levels": LEVELS}
+    base = yml_kwargs(args.ref, "conf/base.yml")
+    k24 = yml_kwargs(args.ref, "conf/base_24kbps.yml")
+    cbr = yml_kwargs(args.ref, "conf/original_dac/cbr.yml")
+    a2 = yml_kwargs(args.ref, "conf/vrvq/vrvq_a2.yml")
+    manifest["yml_kwargs"] = {"conf/base.yml": base, "conf/base_24kbps.yml": k24,
+                              "conf/original_dac/cbr.yml": cbr, "conf/vrvq/vrvq_a2.yml": a2}
+    model_fixture(DAC, ref_utils, base, 2, "golden_nq8", manifest)
+    model_fixture(DAC, ref_utils, k24, 1, "golden_nq28", manifest)
+    k32 = dict(k24, n_codebooks=32)
+    model_fixture(DAC, ref_utils, k32, 1, "golden_nq32", manifest)
+    model_fixture(DAC, ref_utils, cbr, 1, "golden_cbr", manifest, full_z=False)
+    model_fixture(DAC, ref_utils, cbr, 1, "golden_cbr_n4", manifest, n_quantizers=4, full_z=False)
+    rvq_stress_fixture(DAC, base, "golden_rvq_stress_nq8", manifest)
+    rvq_stress_fixture(DAC, k32, "golden_rvq_stress_nq32", manifest, batch=2, frames=40, seed=11)
+    mask_kat(ref_utils, manifest)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, default=float)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,67 @@
+"""The C-ABI library (no GPU needed): it loads, exports every function include/vrvq.h declares,
+the ctypes table matches the header, and host-side argument checks reject bad calls before
+any launch."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from vrvq_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "vrvq.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"(?:const\s+char\s*\*|int)\s+(vrvq_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        decls[m.group(1)] = args
+    return decls
+
+
+def test_header_parsed():
+    decls = header_functions()
+    assert "vrvq_rvq_codes" in decls and "vrvq_conv1d" in decls and len(decls) >= 16
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+
+
+def test_ctypes_table_matches_header():
+    decls = header_functions()
+    for name, args in decls.items():
+        if name in _lib.SIGNATURES:
+            assert len(_lib.SIGNATURES[name]) == len(args), name
+        else:
+            assert name in _lib.EXTRA, f"{name} declared but not bound"
+            assert len(_lib.EXTRA[name][0]) == len(args), name
+    assert set(_lib.SIGNATURES) | set(_lib.EXTRA) == set(decls)
+
+
+def test_status_strings_and_version():
+    lib = _lib.load()
+    assert lib.vrvq_status_string(0) == b"ok"
+    assert b"invalid argument" in lib.vrvq_status_string(10001)
+    assert lib.vrvq_version() >= 100
+
+
+def test_argument_errors_raise_before_launch():
+    lib = _lib.load()
+    # null pointers -> VRVQ_ERR_ARG, returned by the host-side check (no GPU touched)
+    assert lib.vrvq_weight_norm(None, None, 4, 4, None, None) == 10001
+    assert lib.vrvq_conv1d(None, 1, 1, 8, None, None, None, 1, 128, 3, 1, 1, 1, None, None, 0,
+                           None, 8, None) == 10001
+    assert lib.vrvq_rvq_codes(*([None] + [1] * 6 + [None] * 12)) == 10001
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
+    # geometry mismatch (tout inconsistent with the conv formula)
+    p = ctypes.c_void_p(16)
+    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, 4, 128, 7, 1, 3, 1, None, None, 0,
+                           p, 99, None) == 10001

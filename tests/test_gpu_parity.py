@@ -1,0 +1,281 @@
+"""HIP path (through the C-ABI) against the reference's golden fixtures, the CPU oracle and a
+plain PyTorch fp32 reference of each conv kernel. Needs an MI355X.
+
+Bar (north_star): integer codes and masks bit-exact; z_q / latents / waveform within 1e-4
+relative (max-abs normalised)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import vrvq_amd
+from conftest import load_golden, rel_err
+from oracle.vrvq_oracle import Oracle
+from vrvq_amd import ops
+from vrvq_amd.recipe import load_recipe, recipe_state_dict, shapes_of, synthetic_audio
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+DEV = torch.device("cuda:0")
+
+_models = {}
+
+
+def model_for(manifest, name):
+    m = manifest[name]
+    key = (tuple(sorted((k, str(v)) for k, v in m["kwargs"].items())), m["weight_seed"])
+    if key not in _models:
+        model = vrvq_amd.DAC_VRVQ(**m["kwargs"])
+        load_recipe(model, m["weight_seed"])
+        _models[key] = model.to(DEV).eval()
+    return _models[key]
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def test_native_library_loaded():
+    from vrvq_amd import _lib
+    _lib.load()
+    maps = open("/proc/self/maps").read()
+    assert "libvrvq_hip.so" in maps
+
+
+# ------------------------------------------------------------------ whole model vs reference
+@pytest.mark.parametrize("name", ["golden_nq8", "golden_nq28", "golden_nq32", "golden_cbr",
+                                  "golden_cbr_n4"])
+def test_model_forward_vs_reference(manifest, name):
+    m = manifest[name]
+    g = load_golden(name)
+    model = model_for(manifest, name)
+    with torch.no_grad():
+        if m["kwargs"].get("model_type", "VBR") == "VBR":
+            out = model(t(g["audio_in"]), 44100, m["n_quantizers"], 1)
+        else:
+            out = model(t(g["audio_in"]), 44100, m["n_quantizers"])
+    np.testing.assert_array_equal(out["codes"].cpu().numpy(), g["codes"])
+    assert rel_err(out["latents"].cpu().numpy(), g["latents"]) < TOL
+    assert rel_err(out["z"].cpu().numpy(), g["z_q"]) < TOL
+    assert rel_err(out["audio"].cpu().numpy(), g["audio_out"]) < TOL
+    assert float(out["vq/commitment_loss"]) == pytest.approx(float(g["commitment_loss"]), rel=TOL)
+    assert float(out["vq/codebook_loss"]) == pytest.approx(float(g["codebook_loss"]), rel=TOL)
+    if "imp_map" in g:
+        assert rel_err(out["imp_map"].cpu().numpy(), g["imp_map"]) < TOL
+        np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), g["mask_imp"])
+
+
+@pytest.mark.parametrize("name", ["golden_nq8", "golden_nq28"])
+def test_encoder_and_decoder_units(manifest, name):
+    g = load_golden(name)
+    model = model_for(manifest, name)
+    with torch.no_grad():
+        x = model.preprocess(t(g["audio_in"]), 44100)
+        z, feat = model.encoder(x, return_feat=True)
+        assert rel_err(z.cpu().numpy(), g["z"]) < TOL
+        assert rel_err(feat.cpu().numpy(), g["feat"]) < TOL
+        y = model.decode(t(g["z_q"]))[..., :44100]
+    assert rel_err(y.cpu().numpy(), g["audio_out"]) < TOL
+
+
+@pytest.mark.parametrize("name", ["golden_nq8", "golden_nq28", "golden_nq32", "golden_rvq_stress_nq8",
+                                  "golden_rvq_stress_nq32"])
+def test_rvq_unit_vs_reference(manifest, name):
+    """Quantizer fed the reference's own z / feat: isolates the RVQ kernels' numerics."""
+    g = load_golden(name)
+    model = model_for(manifest, name)
+    with torch.no_grad():
+        out = model.quantizer(t(g["z"]), None, t(g["feat"]), 1)
+    np.testing.assert_array_equal(out["codes"].cpu().numpy(), g["codes"])
+    np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), g["mask_imp"])
+    assert rel_err(out["z_q"].cpu().numpy(), g["z_q"]) < TOL
+    assert rel_err(out["latents"].cpu().numpy(), g["latents"]) < TOL
+    assert rel_err(out["imp_map"].cpu().numpy(), g["imp_map"]) < TOL
+    assert rel_err(out["z_q_is"].norm(dim=(2, 3)).cpu().numpy(), g["z_q_is_norm"]) < TOL
+    if "z_q_is_s16" in g:
+        assert rel_err(out["z_q_is"][:, :, ::16, :].cpu().numpy(), g["z_q_is_s16"]) < TOL
+
+
+def test_level_sweep_vs_reference(manifest):
+    """scripts/inference.py:88-112 on the GPU: masks bit-exact, recon within 1e-4, bpf/kbps."""
+    g = load_golden("golden_nq8")
+    model = model_for(manifest, "golden_nq8")
+    res = vrvq_amd.level_sweep(model, t(g["audio_in"]), manifest["levels"])
+    for li, r in enumerate(res):
+        np.testing.assert_array_equal(r["mask"].cpu().numpy(), g[f"sweep{li}_mask"])
+        assert rel_err(r["z_q"].norm(dim=1).cpu().numpy(), g[f"sweep{li}_zq_norm"]) < TOL
+        assert rel_err(r["recon"][..., ::8].cpu().numpy(), g[f"sweep{li}_recon_s8"]) < TOL
+        assert r["bpf"] == pytest.approx(float(g[f"sweep{li}_bpf"]), rel=1e-6)
+        assert r["kbps"] == pytest.approx(float(g[f"sweep{li}_kbps"]), rel=1e-6)
+
+
+def test_mask_kat(manifest):
+    kat = manifest["mask_kat"]
+    s = t(np.asarray(kat["s"], np.float32).reshape(1, 1, -1))
+    for nq in (8, 28, 32):
+        r = kat["results"][str(nq)]
+        mask = vrvq_amd.generate_mask_hard(s, nq)
+        np.testing.assert_array_equal(mask[0].cpu().numpy(), np.asarray(r["mask"], np.float32))
+        assert vrvq_amd.cal_bpf_from_mask(mask, [10] * nq) == pytest.approx(r["bpf10"], rel=1e-7)
+    ste = vrvq_amd.generate_mask_ste(s, 8, alpha=2.0)
+    np.testing.assert_array_equal(ste[0].cpu().numpy(), np.asarray(kat["results"]["ste8_alpha2"], np.float32))
+
+
+# ------------------------------------------------------------------ kernels vs torch fp32
+def _snake_ref(x, alpha):
+    a = alpha.reshape(1, -1, 1)
+    return x + (a + 1e-9).reciprocal() * torch.sin(a * x).pow(2)
+
+
+CONV_CASES = [
+    # (B, cin, cout, T, k, stride, pad, dil, snake, residual, epi)
+    (2, 64, 64, 1000, 7, 1, 3, 1, True, False, 0),
+    (2, 64, 64, 1000, 7, 1, 9, 3, True, False, 0),
+    (2, 96, 96, 777, 7, 1, 27, 9, True, False, 0),
+    (3, 64, 64, 513, 1, 1, 0, 1, True, True, 0),
+    (2, 1, 64, 700, 7, 1, 3, 1, False, False, 0),
+    (2, 64, 128, 1024, 4, 2, 1, 1, True, False, 0),
+    (2, 128, 256, 512, 8, 4, 2, 1, True, False, 0),
+    (2, 256, 512, 256, 16, 8, 4, 1, True, False, 0),
+    (2, 1024, 1024, 87, 3, 1, 1, 1, True, False, 0),
+    (2, 96, 1, 1000, 7, 1, 3, 1, True, False, 1),
+    (2, 8, 1, 87, 3, 1, 1, 1, True, False, 2),
+    (2, 32, 8, 87, 3, 1, 1, 1, True, False, 0),
+    (1, 1024, 1536, 87, 7, 1, 3, 1, False, False, 0),
+    (1, 768, 768, 5, 7, 1, 3, 1, True, True, 0),
+    (1, 16, 16, 1, 7, 1, 3, 1, True, False, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv1d_vs_torch(case):
+    B, cin, cout, T, k, s, p, d, use_snake, use_res, epi = case
+    gen = torch.Generator(device="cpu").manual_seed(hash(case) & 0xFFFF)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cout, cin, k, generator=gen) / np.sqrt(cin * k)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    tout = (T + 2 * p - d * (k - 1) - 1) // s + 1
+    res = (torch.randn(B, cout, tout, generator=gen)).to(DEV) if use_res else None
+    xin = _snake_ref(x, alpha) if use_snake else x
+    ref = F.conv1d(xin.double(), w.double(), b.double(), stride=s, padding=p, dilation=d)
+    if use_res:
+        ref = res.double() + ref
+    ref = [ref, torch.tanh(ref), torch.sigmoid(ref)][epi]
+    wp, cout_pad = ops.pack_conv1d_weight(w)
+    y = ops.conv1d(x, wp, cout, cout_pad, k, s, p, d, bias=b,
+                   alpha=alpha if use_snake else None,
+                   inv_alpha=ops.snake_inv_alpha(alpha) if use_snake else None,
+                   residual=res, epilogue=epi)
+    assert y.shape == ref.shape
+    assert rel_err(y.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8), (2, 384, 192, 333, 4),
+                                  (2, 192, 96, 1000, 2), (1, 16, 8, 1, 2), (1, 64, 32, 3, 8)])
+def test_conv_transpose1d_vs_torch(case):
+    B, cin, cout, T, s = case
+    gen = torch.Generator(device="cpu").manual_seed(s * 1000 + T)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cin, cout, 2 * s, generator=gen) / np.sqrt(cin * 2)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    ref = F.conv_transpose1d(_snake_ref(x, alpha).double(), w.double(), b.double(), stride=s,
+                             padding=(s + 1) // 2)
+    wp, cout_pad = ops.pack_convt1d_weight(w, s)
+    y = ops.conv_transpose1d(x, wp, cout, cout_pad, s, bias=b, alpha=alpha,
+                             inv_alpha=ops.snake_inv_alpha(alpha))
+    assert y.shape == ref.shape
+    assert rel_err(y.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+def test_weight_norm_and_codebook_prep_vs_torch():
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    v = torch.randn(300, 64, 7, generator=gen).to(DEV)
+    g = torch.rand(300, 1, 1, generator=gen).to(DEV) + 0.5
+    w = ops.weight_norm(g, v)
+    ref = v.double() * (g.double() / v.double().norm(dim=(1, 2), keepdim=True))
+    assert rel_err(w.cpu().numpy(), ref.cpu().numpy()) < 1e-6
+    cb = torch.randn(3, 1024, 8, generator=gen).to(DEV)
+    cbn, c2 = ops.codebook_prep(cb)
+    rn = F.normalize(cb.double(), dim=-1)
+    assert rel_err(cbn.cpu().numpy(), rn.cpu().numpy()) < 1e-6
+    assert rel_err(c2.cpu().numpy(), rn.pow(2).sum(-1).cpu().numpy()) < 1e-6
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_full_size_properties(manifest):
+    """BASELINE config 2 (B=32, 8 cb): size-independent invariants of the RVQ outputs, plus
+    oracle agreement on a frame subset."""
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(32, 44100, seed=4321))
+    with torch.no_grad():
+        x = model.preprocess(audio, 44100)
+        z, feat = model.encoder(x, return_feat=True)
+        out = model.quantizer(z, None, feat, 1)
+    codes, mask, zqis = out["codes"], out["mask_imp"], out["z_q_is"]
+    assert codes.shape == (32, 8, 87) and codes.min() >= 0 and codes.max() < 1024
+    assert torch.all(mask[:, 0] == 1)                               # s >= 0 always keeps codebook 0
+    assert torch.all(mask[:, 1:] <= mask[:, :-1])                   # monotone in codebook index
+    zq2 = vrvq_amd.masked_sum(zqis, mask)
+    assert torch.equal(zq2, out["z_q"])                             # same accumulation order
+    # oracle on two clips of the GPU's own latents
+    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **manifest["golden_nq8"]["kwargs"])
+    sel = [0, 31]
+    q = o.quantize(z[sel].cpu().numpy(), None, feat[sel].cpu().numpy(), 1.0)
+    np.testing.assert_array_equal(codes[sel].cpu().numpy(), q["codes"])
+    np.testing.assert_array_equal(mask[sel].cpu().numpy(), q["mask_imp"])
+    assert rel_err(out["z_q"][sel].cpu().numpy(), q["z_q"]) < TOL
+
+
+def test_rvq_big_batch_nq32_vs_oracle(manifest):
+    """BASELINE config 3 shape (B=64, 32 cb) on random latents vs the oracle."""
+    model = model_for(manifest, "golden_nq32")
+    gen = torch.Generator(device="cpu").manual_seed(77)
+    z = torch.randn(64, 1024, 87, generator=gen) * 0.3
+    feat = torch.randn(64, 1024, 87, generator=gen) * 0.3
+    with torch.no_grad():
+        out = model.quantizer(z.to(DEV), None, feat.to(DEV), 1)
+    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **manifest["golden_nq32"]["kwargs"])
+    q = o.quantize(z.numpy(), None, feat.numpy(), 1.0)
+    codes = out["codes"].cpu().numpy()
+    agree = (codes == q["codes"]).mean()
+    assert agree == 1.0, f"codes agreement {agree}"
+    np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), q["mask_imp"])
+    assert rel_err(out["z_q"].cpu().numpy(), q["z_q"]) < TOL
+
+
+@pytest.mark.parametrize("length", [1, 511, 512, 513, 3000])
+def test_ragged_lengths_vs_oracle(manifest, length):
+    model = model_for(manifest, "golden_nq8")
+    audio = synthetic_audio(1, length, seed=length)
+    with torch.no_grad():
+        out = model(t(audio), 44100, None, 1)
+    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **manifest["golden_nq8"]["kwargs"])
+    ref = o.forward(audio, None, 1.0)
+    np.testing.assert_array_equal(out["codes"].cpu().numpy(), ref["codes"])
+    assert out["audio"].shape[-1] == length
+    assert rel_err(out["audio"].cpu().numpy(), ref["audio"]) < TOL
+
+
+def test_deterministic(manifest):
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(4, 44100, seed=9))
+    with torch.no_grad():
+        a = model(audio, 44100, None, 1)
+        b = model(audio, 44100, None, 1)
+    for k in ("audio", "z", "codes", "latents", "mask_imp"):
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_cbr_mode_of_vbr_model(manifest):
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(1, 44100, seed=3))
+    with torch.no_grad():
+        x = model.preprocess(audio, 44100)
+        out = model.encode(x, n_quantizers=8)
+        assert out["imp_map"] is None and torch.all(out["mask_imp"] == 1)
+        with pytest.raises(RuntimeError):
+            model.encode(x, n_quantizers=4)

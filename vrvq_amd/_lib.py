@@ -1,0 +1,74 @@
+"""ctypes binding of the C-ABI in include/vrvq.h (libvrvq_hip.so, built in-tree for gfx950).
+
+The library is the product: every arithmetic op of the hot path runs in it. There is no
+fallback — if the library is missing or a call fails, a RuntimeError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_NAME = "libvrvq_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+# name -> argtypes (restype is int status unless noted). Mirrors include/vrvq.h exactly;
+# tests/test_capi.py checks this table against the header and the exported symbols.
+SIGNATURES = {
+    "vrvq_weight_norm": [_P, _P, _I, _I, _P, _P],
+    "vrvq_snake_inv_alpha": [_P, _I, _P, _P],
+    "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
+    "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
+    "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
+    "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
+    "vrvq_rvq_codes": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "vrvq_rvq_expand": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
+    "vrvq_masked_loss": [_P, _P, _I, _I, _I, _P, _P],
+    "vrvq_mask_hard": [_P, _I, _I, _I, _P, _P],
+    "vrvq_scale_imp": [_P, _I, _F, _F, _P, _P],
+    "vrvq_masked_sum": [_P, _P, _I, _I, _I, _I, _P, _P],
+    "vrvq_bpf": [_P, _P, _I, _I, _I, _P, _P],
+}
+EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libvrvq_hip.so (once). Raises RuntimeError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"vrvq_amd: HIP library {LIB_PATH} is missing; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = _I
+        for name, (argtypes, restype) in EXTRA.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a C-ABI entry point; raise RuntimeError with the library's message on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.vrvq_status_string(rc)
+        raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else 'unknown'}")

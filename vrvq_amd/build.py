@@ -1,0 +1,56 @@
+"""Build libvrvq_hip.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the
+repo snapshot to the GPU box)."""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libvrvq_hip.so")
+ARCH = os.environ.get("VRVQ_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}",
+         "-Wall", "-Wno-unused-function"]
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def deps():
+    return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [
+        os.path.join(REPO, "include", "vrvq.h"), os.path.abspath(__file__)]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in deps())
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build vrvq_amd)")
+
+
+def build_library(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(REPO, "include"), "-o", tmp] + sources()
+    if verbose:
+        print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build_library(force="--force" in sys.argv)

@@ -1,0 +1,58 @@
+"""YAML config loading with the reference's argbind conventions (conf/*.yml).
+
+Supported: `$include` lists (included files load first, in order; the including file's keys
+override; values replace wholesale), `DAC_VRVQ.<kwarg>` keys -> DAC_VRVQ constructor kwargs
+(scripts/train.py:46, scripts/inference.py:24). Include paths are resolved relative to the
+current directory first (argbind's behaviour), then relative to the including file's
+directory and its parents.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict
+
+import yaml
+
+MODEL_PREFIX = "DAC_VRVQ."
+
+
+def _resolve(path: str, base_dir: str) -> str:
+    if os.path.isabs(path) or os.path.exists(path):
+        return path
+    d = os.path.abspath(base_dir)
+    while True:
+        cand = os.path.join(d, path)
+        if os.path.exists(cand):
+            return cand
+        parent = os.path.dirname(d)
+        if parent == d:
+            raise FileNotFoundError(f"config include not found: {path} (from {base_dir})")
+        d = parent
+
+
+def load_config(path: str, _seen=None) -> Dict[str, Any]:
+    _seen = set() if _seen is None else _seen
+    path = os.path.abspath(path)
+    if path in _seen:
+        raise ValueError(f"config include cycle at {path}")
+    _seen = _seen | {path}
+    with open(path) as f:
+        data = yaml.safe_load(f) or {}
+    merged: Dict[str, Any] = {}
+    for inc in data.pop("$include", []) or []:
+        merged.update(load_config(_resolve(inc, os.path.dirname(path)), _seen))
+    merged.update(data)
+    return merged
+
+
+def model_kwargs(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    return {k[len(MODEL_PREFIX):]: v for k, v in cfg.items() if k.startswith(MODEL_PREFIX)}
+
+
+def from_config(path: str, **overrides):
+    """Construct a DAC_VRVQ from a conf/*.yml file (plus keyword overrides)."""
+    from .model import DAC_VRVQ
+
+    kw = model_kwargs(load_config(path))
+    kw.update(overrides)
+    return DAC_VRVQ(**kw)

@@ -1,0 +1,48 @@
+// Shared helpers for the gfx950 VRVQ kernels. Compiled with -ffp-contract=off: every fused
+// multiply-add in the product path is written explicitly (fmaf / MFMA) so two kernels that
+// must agree bit-for-bit (rvq codes vs expand) evaluate the same expression tree.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/vrvq.h"
+
+#define VRVQ_CHECK_ARG(cond)            \
+  do {                                  \
+    if (!(cond)) return VRVQ_ERR_ARG;   \
+  } while (0)
+
+static inline int vrvq_launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Snake activation, models/layers.py:30: x + (alpha + 1e-9)^-1 * sin(alpha * x)^2.
+// Evaluated as the reference's op sequence (mul, sin, square, mul, add), one rounding each.
+__device__ __forceinline__ float snake_act(float v, float alpha, float inv_alpha) {
+  const float s = sinf(alpha * v);
+  return v + inv_alpha * (s * s);
+}
+
+// 8-term dot product in k order (fmaf chain); used for in_proj/out_proj/codebook distance.
+__device__ __forceinline__ float dot8(const float4& a0, const float4& a1, const float4& b0,
+                                      const float4& b1) {
+  float acc = a0.x * b0.x;
+  acc = fmaf(a0.y, b0.y, acc);
+  acc = fmaf(a0.z, b0.z, acc);
+  acc = fmaf(a0.w, b0.w, acc);
+  acc = fmaf(a1.x, b1.x, acc);
+  acc = fmaf(a1.y, b1.y, acc);
+  acc = fmaf(a1.z, b1.z, acc);
+  acc = fmaf(a1.w, b1.w, acc);
+  return acc;
+}
+
+// out_proj of one frame for one output channel: (W_out[c,:] . zst) + b_out[c].
+// Shared by vrvq_rvq_codes (residual update) and vrvq_rvq_expand (z_q_is), so both
+// produce the same bits.
+__device__ __forceinline__ float out_proj1(const float4& w0, const float4& w1, float bias,
+                                           const float4& z0, const float4& z1) {
+  return dot8(w0, w1, z0, z1) + bias;
+}

@@ -1,0 +1,337 @@
+// Snake-fused 1-D convolution and polyphase transposed convolution for gfx950.
+//
+// Implicit GEMM:  Y[M x N] = W[M x K] * Xs[K x N]
+//   M = output channels (or phase-channels for the transposed conv), N = output time,
+//   K = Cin * taps, Xs = im2col(snake(x)) never materialised: each workgroup stages a
+//   [CK channels x (BN*stride + halo)] window of snake(x) in LDS once per K-chunk and the
+//   B-operand of every tap is read from that window at offset (j*stride + tap*dil).
+// MFMA: v_mfma_f32_32x32x2_f32 (exact fp32, k-ordered fmaf chain, 64 cyc/SIMD issue).
+//   A (32x2):  lane l holds W[m = l&31][k = l>>5]
+//   B (2x32):  lane l holds Xs[k = l>>5][n = l&31]
+//   D (32x32): lane l, reg r holds Y[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31]
+// So each store instruction writes 32 consecutive time steps (128 B) per row.
+//
+// Reference semantics: models/layers.py:17-41 (WNConv1d, WNConvTranspose1d, snake),
+// :52-110 (ResidualUnit skip, EncoderBlock, DecoderBlock), models/dac_vrvq.py:19-80,
+// models/importance_subnet.py:38-45.
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+struct ConvArgs {
+  const float* x;          // [B][cin][tin]
+  const float* alpha;      // [cin] or null
+  const float* inv_alpha;  // [cin]
+  const float* w;          // [cin][KS][m_pad]
+  const float* bias;       // [cout] or null
+  const float* res;        // [B][cout][ylen] or null
+  float* y;                // [B][cout][ylen]
+  int cin, tin;
+  int M;                   // GEMM rows: cout (normal) or cout*up (transposed)
+  int m_pad;
+  int cout;
+  int stride, pad, dil;
+  int ng;                  // GEMM columns (output positions of the GEMM)
+  int up, up_pad;          // transposed conv: upsample factor and its padding (0 = normal)
+  int ylen;                // output row length
+  int epi;
+  int n_mt, n_nt;          // M tiles, N tiles
+};
+
+template <int KS>
+struct ChunkCfg {
+  // Input channels per K-chunk: keep CK*KS ~ 32..64 rows of W per stage.
+  static constexpr int CK = KS == 1 ? 32 : KS <= 4 ? 16 : KS <= 8 ? 8 : 4;
+};
+
+__device__ __forceinline__ float apply_epi(float v, int epi) {
+  if (epi == VRVQ_EPI_TANH) return tanhf(v);
+  if (epi == VRVQ_EPI_SIGMOID) return 1.0f / (1.0f + expf(-v));
+  return v;
+}
+
+template <int BM, int BN, int WM, int KS>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM;
+  constexpr int TN = BN / WN;
+  constexpr int RM = TM / 32;
+  constexpr int RN = TN / 32;
+  constexpr int CK = ChunkCfg<KS>::CK;
+  constexpr int KROWS = CK * KS;
+  static_assert(RM >= 1 && RN >= 1 && TM % 32 == 0 && TN % 32 == 0, "tile");
+  static_assert(CK % 2 == 0, "CK even");
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* ws = smem;                 // [KROWS][BM]
+  float* xs = smem + KROWS * BM;    // [CK][XWP]
+  const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
+  const int XWP = (XW + 3) & ~3;
+
+  int bid = blockIdx.x;
+  const int mt = bid % a.n_mt;
+  bid /= a.n_mt;
+  const int nt = bid % a.n_nt;
+  const int b = bid / a.n_nt;
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int lr = lane & 31;
+  const int lh = lane >> 5;
+
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  const int xbase = n0 * a.stride - a.pad;
+
+  for (int ci0 = 0; ci0 < a.cin; ci0 += CK) {
+    // ---- stage W chunk: rows (ci0*KS .. ci0*KS+KROWS) x cols [m0, m0+BM), float4 ----
+    for (int i = tid; i < KROWS * (BM / 4); i += 256) {
+      const int rr = i / (BM / 4);
+      const int cc = (i - rr * (BM / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ci0 + rr / KS < a.cin)
+        v = *reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc);
+      *reinterpret_cast<float4*>(ws + rr * BM + cc) = v;
+    }
+    // ---- stage snake(x) window: CK rows x XW positions (zero outside [0, tin)) ----
+    for (int cl = wave; cl < CK; cl += 4) {
+      const int ci = ci0 + cl;
+      const bool cvalid = ci < a.cin;
+      float al = 0.f, ia = 0.f;
+      const bool sn = cvalid && a.alpha != nullptr;
+      if (sn) {
+        al = a.alpha[ci];
+        ia = a.inv_alpha[ci];
+      }
+      const float* xr = xb + (size_t)(cvalid ? ci : 0) * a.tin;
+      for (int p = lane; p < XWP; p += 64) {
+        const int t = xbase + p;
+        float v = 0.f;
+        if (cvalid && p < XW && t >= 0 && t < a.tin) {
+          v = xr[t];
+          if (sn) v = snake_act(v, al, ia);
+        }
+        xs[cl * XWP + p] = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- MFMA over the chunk: K order = (tap, channel pair) ----
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int cc = 0; cc < CK; cc += 2) {
+        const int kr = cc + lh;
+        float av[RM], bv[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) av[i] = ws[(kr * KS + k) * BM + wm * TM + i * 32 + lr];
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          bv[j] = xs[kr * XWP + (wn * TN + j * 32 + lr) * a.stride + k * a.dil];
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias, residual, activation, store ----
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn * TN + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= a.M || n >= a.ng) continue;
+        int co, t;
+        if (a.up == 0) {
+          co = m;
+          t = n;
+        } else {
+          co = m / a.up;
+          t = n * a.up + (m - co * a.up) - a.up_pad;
+          if (t < 0 || t >= a.ylen) continue;
+        }
+        float v = acc[i][j][r];
+        if (a.bias) v = v + a.bias[co];
+        const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
+        if (a.res) v = a.res[o] + v;
+        a.y[o] = apply_epi(v, a.epi);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int KS>
+int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
+  ConvArgs a = a0;
+  a.n_mt = (a.M + BM - 1) / BM;
+  a.n_nt = (a.ng + BN - 1) / BN;
+  if (a.m_pad < a.n_mt * BM) return VRVQ_ERR_ARG;
+  constexpr int CK = ChunkCfg<KS>::CK;
+  const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
+  const int XWP = (XW + 3) & ~3;
+  const size_t lds = (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
+  if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, KS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const long long nblk = (long long)a.n_mt * a.n_nt * batch;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, KS>), dim3((unsigned)nblk), dim3(256), lds,
+                     st, a);
+  return vrvq_launch_status();
+}
+
+// Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
+template <int KS>
+int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
+  auto waste = [&](int bn) { return ((a.ng + bn - 1) / bn) * bn - a.ng; };
+  int bn;
+  if (a.ng <= 32) bn = 32;
+  else {
+    bn = 128;
+    // Prefer a narrower tile only if it removes a clearly larger share of padding.
+    if (waste(64) * 10 < waste(128) * 7 && a.ng < 4096) bn = 64;
+    if (a.ng <= 128 && waste(32) * 10 < waste(bn) * 7) bn = 32;
+  }
+  if (a.M <= 32) return launch_cfg<32, 128, 1, KS>(a, batch, st);
+  if (bn == 32) return launch_cfg<128, 32, 4, KS>(a, batch, st);
+  if (a.M <= 64) {
+    if (bn == 64) return launch_cfg<64, 64, 2, KS>(a, batch, st);
+    return launch_cfg<64, 128, 2, KS>(a, batch, st);
+  }
+  if (bn == 64) return launch_cfg<128, 64, 2, KS>(a, batch, st);
+  return launch_cfg<128, 128, 2, KS>(a, batch, st);
+}
+
+int dispatch_ks(int ks, const ConvArgs& a, int batch, hipStream_t st) {
+  switch (ks) {
+    case 1: return dispatch_tiles<1>(a, batch, st);
+    case 2: return dispatch_tiles<2>(a, batch, st);
+    case 3: return dispatch_tiles<3>(a, batch, st);
+    case 4: return dispatch_tiles<4>(a, batch, st);
+    case 7: return dispatch_tiles<7>(a, batch, st);
+    case 8: return dispatch_tiles<8>(a, batch, st);
+    case 16: return dispatch_tiles<16>(a, batch, st);
+    default: return VRVQ_ERR_UNSUPPORTED;
+  }
+}
+
+__global__ void pack_conv1d_kernel(const float* __restrict__ w, int cout, int cin, int k,
+                                   int cout_pad, float* __restrict__ wp) {
+  const size_t total = (size_t)cin * k * cout_pad;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i % cout_pad);
+    const size_t rk = i / cout_pad;
+    const int kk = (int)(rk % k);
+    const int ci = (int)(rk / k);
+    wp[i] = co < cout ? w[((size_t)co * cin + ci) * k + kk] : 0.0f;
+  }
+}
+
+// Polyphase layout: wp[ci][tap][co*s + r]; tap 1 <-> x[m] (kernel index r),
+// tap 0 <-> x[m-1] (kernel index r + s).
+__global__ void pack_convt1d_kernel(const float* __restrict__ w, int cin, int cout, int s,
+                                    int cout_pad, float* __restrict__ wp) {
+  const size_t total = (size_t)cin * 2 * cout_pad;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int mm = (int)(i % cout_pad);
+    const size_t rk = i / cout_pad;
+    const int tap = (int)(rk % 2);
+    const int ci = (int)(rk / 2);
+    float v = 0.0f;
+    if (mm < cout * s) {
+      const int co = mm / s, r = mm - co * s;
+      const int kk = tap == 1 ? r : r + s;
+      v = w[((size_t)ci * cout + co) * (2 * s) + kk];
+    }
+    wp[i] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
+                           const float* inv_alpha, const float* w_packed, int cout,
+                           int cout_pad, int k, int stride, int pad, int dil, const float* bias,
+                           const float* residual, int epilogue, float* y, int tout,
+                           vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && w_packed && y);
+  VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && stride > 0 &&
+                 dil > 0 && pad >= 0 && tout > 0);
+  VRVQ_CHECK_ARG(cout_pad >= cout && cout_pad % 128 == 0);
+  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
+  VRVQ_CHECK_ARG(epilogue >= 0 && epilogue <= 2);
+  const long long expect = ((long long)tin + 2LL * pad - (long long)dil * (k - 1) - 1) / stride + 1;
+  VRVQ_CHECK_ARG(expect == tout);
+  ConvArgs a{};
+  a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
+  a.res = residual; a.y = y;
+  a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
+  a.stride = stride; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0;
+  a.ylen = tout; a.epi = epilogue;
+  return dispatch_ks(k, a, batch, as_stream(stream));
+}
+
+extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin,
+                                     const float* alpha, const float* inv_alpha,
+                                     const float* w_packed, int cout, int cout_pad, int stride,
+                                     const float* bias, float* y, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && w_packed && y);
+  VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && stride > 0);
+  VRVQ_CHECK_ARG(cout_pad >= cout * stride && cout_pad % 128 == 0);
+  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
+  const int p = (stride + 1) / 2;  // math.ceil(stride / 2), models/layers.py:102
+  ConvArgs a{};
+  a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
+  a.res = nullptr; a.y = y;
+  a.cin = cin; a.tin = tin; a.M = cout * stride; a.m_pad = cout_pad; a.cout = cout;
+  a.stride = 1; a.pad = 1; a.dil = 1; a.ng = tin + 1; a.up = stride; a.up_pad = p;
+  a.ylen = (tin - 1) * stride - 2 * p + 2 * stride;
+  a.epi = VRVQ_EPI_NONE;
+  return dispatch_ks(2, a, batch, as_stream(stream));
+}
+
+extern "C" int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
+                                       float* w_packed, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w && w_packed && cout > 0 && cin > 0 && k > 0 && cout_pad >= cout);
+  const size_t total = (size_t)cin * k * cout_pad;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(pack_conv1d_kernel, dim3(grid), dim3(256), 0, as_stream(stream), w, cout,
+                     cin, k, cout_pad, w_packed);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_pack_convt1d_weight(const float* w, int cin, int cout, int stride,
+                                        int cout_pad, float* w_packed, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w && w_packed && cout > 0 && cin > 0 && stride > 0 && cout_pad >= cout * stride);
+  const size_t total = (size_t)cin * 2 * cout_pad;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(pack_convt1d_kernel, dim3(grid), dim3(256), 0, as_stream(stream), w, cin,
+                     cout, stride, cout_pad, w_packed);
+  return vrvq_launch_status();
+}

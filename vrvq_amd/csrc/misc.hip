@@ -1,0 +1,217 @@
+// Weight preparation, importance gating and small reductions for the VRVQ hot path.
+#include "common.h"
+
+namespace {
+
+// One workgroup per row: w = v * (g / ||v||) (torch._weight_norm, dim = 0).
+__global__ __launch_bounds__(256) void weight_norm_kernel(const float* __restrict__ g,
+                                                          const float* __restrict__ v, int cols,
+                                                          float* __restrict__ w) {
+  __shared__ float part[256];
+  const size_t row = blockIdx.x;
+  const float* vr = v + row * cols;
+  float ss = 0.0f;
+  for (int c = threadIdx.x; c < cols; c += 256) ss = fmaf(vr[c], vr[c], ss);
+  part[threadIdx.x] = ss;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+    __syncthreads();
+  }
+  const float scale = g[row] / sqrtf(part[0]);
+  for (int c = threadIdx.x; c < cols; c += 256) w[row * cols + c] = vr[c] * scale;
+}
+
+__global__ void inv_alpha_kernel(const float* __restrict__ alpha, int n, float* __restrict__ inv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) inv[i] = 1.0f / (alpha[i] + 1e-9f);
+}
+
+__global__ void codebook_prep_kernel(const float* __restrict__ cb, int rows, int dim,
+                                     float* __restrict__ cbn, float* __restrict__ c2) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float* x = cb + (size_t)r * dim;
+  float ss = 0.0f;
+  for (int k = 0; k < dim; ++k) ss = fmaf(x[k], x[k], ss);
+  const float den = fmaxf(sqrtf(ss), 1e-12f);  // F.normalize: x / clamp_min(||x||, eps)
+  float s2 = 0.0f;
+  for (int k = 0; k < dim; ++k) {
+    const float y = x[k] / den;
+    cbn[(size_t)r * dim + k] = y;
+    s2 = fmaf(y, y, s2);
+  }
+  c2[r] = s2;
+}
+
+// out[0] = sum_{b,t} (sum_i loss[b,i,t] * mask[b,i,t]) / (B*T); single workgroup, fixed order.
+__global__ __launch_bounds__(1024) void masked_loss_kernel(const float* __restrict__ loss,
+                                                           const float* __restrict__ mask, int B,
+                                                           int nq, int T, float* __restrict__ out) {
+  __shared__ float part[1024];
+  float acc = 0.0f;
+  const int NF = B * T;
+  for (int n = threadIdx.x; n < NF; n += 1024) {
+    const int b = n / T, t = n - b * T;
+    float s = 0.0f;
+    for (int i = 0; i < nq; ++i) {
+      const size_t o = ((size_t)b * nq + i) * T + t;
+      s = s + loss[o] * (mask ? mask[o] : 1.0f);
+    }
+    acc += s;
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = 512; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = part[0] / (float)NF;
+}
+
+__global__ void mask_hard_kernel(const float* __restrict__ s, int B, int T, int nq,
+                                 float* __restrict__ mask) {
+  const size_t total = (size_t)B * nq * T;
+  for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < total;
+       o += (size_t)gridDim.x * blockDim.x) {
+    const int t = (int)(o % T);
+    const size_t bi = o / T;
+    const int i = (int)(bi % nq);
+    const int b = (int)(bi / nq);
+    mask[o] = (s[(size_t)b * T + t] - (float)i >= 0.0f) ? 1.0f : 0.0f;
+  }
+}
+
+__global__ void scale_imp_kernel(const float* __restrict__ imp, int n, float a, float c,
+                                 float* __restrict__ s) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) s[i] = (imp[i] * a) * c;
+}
+
+// z_q[b, e] = sum_i mask[b,i,t(e)] * z_q_is[b,i,e] over the (D*T) slab, float4 per thread.
+__global__ void masked_sum_kernel(const float* __restrict__ zqis, const float* __restrict__ mask,
+                                  int B, int nq, int D, int T, float* __restrict__ zq) {
+  const size_t slab4 = (size_t)D * T / 4;
+  const size_t total = (size_t)B * slab4;
+  for (size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x; q < total;
+       q += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = q / slab4;
+    const size_t e4 = q - b * slab4;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int tt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tt[k] = (int)((e4 * 4 + k) % T);
+    for (int i = 0; i < nq; ++i) {
+      const float4 v = reinterpret_cast<const float4*>(zqis + ((b * nq + i) * D) * (size_t)T)[e4];
+      const float* mr = mask + (b * nq + i) * (size_t)T;
+      acc[0] = acc[0] + v.x * mr[tt[0]];
+      acc[1] = acc[1] + v.y * mr[tt[1]];
+      acc[2] = acc[2] + v.z * mr[tt[2]];
+      acc[3] = acc[3] + v.w * mr[tt[3]];
+    }
+    reinterpret_cast<float4*>(zq + b * (size_t)D * T)[e4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
+__global__ __launch_bounds__(1024) void bpf_kernel(const float* __restrict__ mask,
+                                                   const float* __restrict__ bits, int B, int nq,
+                                                   int T, float* __restrict__ out) {
+  __shared__ float part[1024];
+  const size_t total = (size_t)B * nq * T;
+  float acc = 0.0f;
+  for (size_t o = threadIdx.x; o < total; o += 1024) {
+    const int i = (int)((o / T) % nq);
+    acc += mask[o] * bits[i];
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = 512; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = part[0] / (float)((size_t)B * T);
+}
+
+unsigned grid_for(size_t total, unsigned block) {
+  size_t g = (total + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g == 0) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+extern "C" const char* vrvq_status_string(int status) {
+  switch (status) {
+    case VRVQ_OK: return "ok";
+    case VRVQ_ERR_ARG: return "vrvq: invalid argument (null pointer, size or shape mismatch)";
+    case VRVQ_ERR_UNSUPPORTED: return "vrvq: shape outside the instantiated kernel set";
+    default: return hipGetErrorString((hipError_t)status);
+  }
+}
+
+extern "C" int vrvq_version(void) { return 100; }
+
+extern "C" int vrvq_weight_norm(const float* g, const float* v, int rows, int cols, float* w,
+                                vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(g && v && w && rows > 0 && cols > 0);
+  hipLaunchKernelGGL(weight_norm_kernel, dim3(rows), dim3(256), 0, as_stream(stream), g, v, cols, w);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv,
+                                    vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(alpha && inv && channels > 0);
+  hipLaunchKernelGGL(inv_alpha_kernel, dim3((channels + 255) / 256), dim3(256), 0,
+                     as_stream(stream), alpha, channels, inv);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_codebook_prep(const float* cb, int rows, int dim, float* cbn, float* c2,
+                                  vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(cb && cbn && c2 && rows > 0 && dim > 0);
+  hipLaunchKernelGGL(codebook_prep_kernel, dim3((rows + 255) / 256), dim3(256), 0,
+                     as_stream(stream), cb, rows, dim, cbn, c2);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_masked_loss(const float* loss_pf, const float* mask, int batch, int nq,
+                                int frames, float* out, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(loss_pf && out && batch > 0 && nq > 0 && frames > 0);
+  hipLaunchKernelGGL(masked_loss_kernel, dim3(1), dim3(1024), 0, as_stream(stream), loss_pf,
+                     mask, batch, nq, frames, out);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_mask_hard(const float* s, int batch, int frames, int nq, float* mask,
+                              vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(s && mask && batch > 0 && frames > 0 && nq > 0);
+  hipLaunchKernelGGL(mask_hard_kernel, dim3(grid_for((size_t)batch * nq * frames, 256)), dim3(256),
+                     0, as_stream(stream), s, batch, frames, nq, mask);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_scale_imp(const float* imp, int n, float a, float c, float* s,
+                              vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(imp && s && n > 0);
+  hipLaunchKernelGGL(scale_imp_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     imp, n, a, c, s);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_masked_sum(const float* z_q_is, const float* mask, int batch, int nq, int dim,
+                               int frames, float* z_q, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(z_q_is && mask && z_q && batch > 0 && nq > 0 && dim > 0 && frames > 0);
+  VRVQ_CHECK_ARG(((size_t)dim * frames) % 4 == 0);
+  hipLaunchKernelGGL(masked_sum_kernel, dim3(grid_for((size_t)batch * dim * frames / 4, 256)),
+                     dim3(256), 0, as_stream(stream), z_q_is, mask, batch, nq, dim, frames, z_q);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_bpf(const float* mask, const float* bits, int batch, int nq, int frames,
+                        float* out, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(mask && bits && out && batch > 0 && nq > 0 && frames > 0);
+  hipLaunchKernelGGL(bpf_kernel, dim3(1), dim3(1024), 0, as_stream(stream), mask, bits, batch, nq,
+                     frames, out);
+  return vrvq_launch_status();
+}

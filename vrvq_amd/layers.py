@@ -1,0 +1,199 @@
+"""NN primitives of the VRVQ codec with the reference's parameter layout, run on gfx950 kernels.
+
+Mirrors models/layers.py (reference): Snake1d (:35-41), WNConv1d (:17-18),
+WNConvTranspose1d (:21-22), ResidualUnit (:52-68), EncoderBlock (:71-89),
+DecoderBlock (:92-110). Parameters keep the reference's names and shapes
+(`weight_g`, `weight_v`, `bias`, `alpha`) so a reference `state_dict` loads with
+`strict=True`; the modules' forward passes go through the fused HIP kernels in `ops`
+(Snake is fused into the following convolution, the residual add into the k=1 conv's
+epilogue). Weight norm is folded once per parameter version, not per forward.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+def _param_key(*ps):
+    return tuple((p.device, p.data_ptr(), p._version) for p in ps)
+
+
+class Snake1d(nn.Module):
+    """Snake activation parameters (models/layers.py:35-41); applied inside the next conv."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.channels = channels
+        self.alpha = nn.Parameter(torch.ones(1, channels, 1))
+        self._cache = None
+
+    def prepared(self):
+        """(alpha[C], 1/(alpha+1e-9)[C]) on the parameter's device."""
+        key = _param_key(self.alpha)
+        if self._cache is None or self._cache[0] != key:
+            a = self.alpha.detach().reshape(-1).contiguous()
+            self._cache = (key, a, ops.snake_inv_alpha(a))
+        return self._cache[1], self._cache[2]
+
+    def forward(self, x):  # standalone use (not on the fused path)
+        raise RuntimeError("Snake1d is fused into the following convolution in vrvq_amd; "
+                           "call the owning block instead")
+
+
+def _wn_init(weight_v: torch.Tensor, fan_in: int, out_dim0: int):
+    # PyTorch default Conv init (kaiming_uniform a=sqrt(5) -> U(-1/sqrt(fan_in), +)),
+    # then weight_norm's g = ||v||: the effective init of the reference (its
+    # trunc_normal_ init_weights is discarded by the weight_norm pre-hook).
+    bound = 1.0 / math.sqrt(fan_in)
+    with torch.no_grad():
+        weight_v.uniform_(-bound, bound)
+        g = weight_v.reshape(out_dim0, -1).norm(dim=1)
+    return g
+
+
+class WNConv1d(nn.Module):
+    """Weight-normalised Conv1d (models/layers.py:17-18), fused Snake prologue."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1,
+                 padding: int = 0, dilation: int = 1):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size = (kernel_size,)
+        self.stride = (stride,)
+        self.padding = (padding,)
+        self.dilation = (dilation,)
+        # Registration order bias, weight_g, weight_v = the reference's state_dict order
+        # (torch weight_norm re-registers g and v after the conv's bias).
+        self.bias = nn.Parameter(torch.zeros(out_channels))  # init_weights zeroes conv biases
+        v = torch.empty(out_channels, in_channels, kernel_size)
+        g = _wn_init(v, in_channels * kernel_size, out_channels)
+        self.weight_g = nn.Parameter(g.reshape(out_channels, 1, 1).clone())
+        self.weight_v = nn.Parameter(v)
+        self._cache = None
+
+    def folded_weight(self) -> torch.Tensor:
+        """w = v * (g / ||v||) in the reference layout (Cout, Cin, k)."""
+        return ops.weight_norm(self.weight_g.detach().contiguous(), self.weight_v.detach().contiguous())
+
+    def prepared(self):
+        key = _param_key(self.weight_g, self.weight_v)
+        if self._cache is None or self._cache[0] != key:
+            wp, cout_pad = ops.pack_conv1d_weight(self.folded_weight())
+            self._cache = (key, wp, cout_pad)
+        return self._cache[1], self._cache[2]
+
+    def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
+                residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE):
+        wp, cout_pad = self.prepared()
+        alpha = inv = None
+        if snake is not None:
+            alpha, inv = snake.prepared()
+        return ops.conv1d(x, wp, self.out_channels, cout_pad, self.kernel_size[0],
+                          self.stride[0], self.padding[0], self.dilation[0],
+                          bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
+                          residual=residual, epilogue=epilogue)
+
+
+class WNConvTranspose1d(nn.Module):
+    """Weight-normalised ConvTranspose1d (models/layers.py:21-22); norm over dim 0 = Cin."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1,
+                 padding: int = 0):
+        super().__init__()
+        if kernel_size != 2 * stride or padding != math.ceil(stride / 2):
+            raise ValueError("WNConvTranspose1d: only the DecoderBlock geometry "
+                             "(kernel 2*stride, padding ceil(stride/2)) is implemented")
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size = (kernel_size,)
+        self.stride = (stride,)
+        self.padding = (padding,)
+        self.dilation = (1,)
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+        v = torch.empty(in_channels, out_channels, kernel_size)
+        g = _wn_init(v, out_channels * kernel_size, in_channels)
+        self.weight_g = nn.Parameter(g.reshape(in_channels, 1, 1).clone())
+        self.weight_v = nn.Parameter(v)
+        self._cache = None
+
+    def folded_weight(self) -> torch.Tensor:
+        return ops.weight_norm(self.weight_g.detach().contiguous(), self.weight_v.detach().contiguous())
+
+    def prepared(self):
+        key = _param_key(self.weight_g, self.weight_v)
+        if self._cache is None or self._cache[0] != key:
+            wp, cout_pad = ops.pack_convt1d_weight(self.folded_weight(), self.stride[0])
+            self._cache = (key, wp, cout_pad)
+        return self._cache[1], self._cache[2]
+
+    def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None):
+        wp, cout_pad = self.prepared()
+        alpha = inv = None
+        if snake is not None:
+            alpha, inv = snake.prepared()
+        return ops.conv_transpose1d(x, wp, self.out_channels, cout_pad, self.stride[0],
+                                    bias=self.bias.detach(), alpha=alpha, inv_alpha=inv)
+
+
+class ResidualUnit(nn.Module):
+    """x + conv1(snake(conv7_dil(snake(x))))  (models/layers.py:52-68)."""
+
+    def __init__(self, dim: int = 16, dilation: int = 1):
+        super().__init__()
+        pad = ((7 - 1) * dilation) // 2
+        self.block = nn.Sequential(
+            Snake1d(dim),
+            WNConv1d(dim, dim, kernel_size=7, dilation=dilation, padding=pad),
+            Snake1d(dim),
+            WNConv1d(dim, dim, kernel_size=1),
+        )
+
+    def forward(self, x):
+        y = self.block[1](x, snake=self.block[0])
+        # "same" padding: the reference's centre crop (:65-67) never triggers.
+        return self.block[3](y, snake=self.block[2], residual=x)
+
+
+class EncoderBlock(nn.Module):
+    """3 residual units (dil 1, 3, 9), Snake, strided conv k=2s (models/layers.py:71-89)."""
+
+    def __init__(self, dim: int = 16, stride: int = 1):
+        super().__init__()
+        self.block = nn.Sequential(
+            ResidualUnit(dim // 2, dilation=1),
+            ResidualUnit(dim // 2, dilation=3),
+            ResidualUnit(dim // 2, dilation=9),
+            Snake1d(dim // 2),
+            WNConv1d(dim // 2, dim, kernel_size=2 * stride, stride=stride,
+                     padding=math.ceil(stride / 2)),
+        )
+
+    def forward(self, x):
+        for i in range(3):
+            x = self.block[i](x)
+        return self.block[4](x, snake=self.block[3])
+
+
+class DecoderBlock(nn.Module):
+    """Snake, ConvTranspose k=2s (x s upsampling), 3 residual units (models/layers.py:92-110)."""
+
+    def __init__(self, input_dim: int = 16, output_dim: int = 8, stride: int = 1):
+        super().__init__()
+        self.block = nn.Sequential(
+            Snake1d(input_dim),
+            WNConvTranspose1d(input_dim, output_dim, kernel_size=2 * stride, stride=stride,
+                              padding=math.ceil(stride / 2)),
+            ResidualUnit(output_dim, dilation=1),
+            ResidualUnit(output_dim, dilation=3),
+            ResidualUnit(output_dim, dilation=9),
+        )
+
+    def forward(self, x):
+        x = self.block[1](x, snake=self.block[0])
+        for i in range(2, 5):
+            x = self.block[i](x)
+        return x

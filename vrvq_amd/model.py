@@ -1,0 +1,410 @@
+"""Drop-in DAC_VRVQ codec (reference: models/dac_vrvq.py, models/quantize.py,
+models/importance_subnet.py, models/dac_base.py) on gfx950 kernels.
+
+Same constructor kwargs (the `DAC_VRVQ.*` keys of conf/*.yml), same state_dict keys, same
+`preprocess / encode / decode / forward` signatures and output dicts. All arithmetic runs in
+libvrvq_hip.so (see ops.py); the modules here hold parameters and orchestrate launches.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .layers import (DecoderBlock, EncoderBlock, ResidualUnit, Snake1d, WNConv1d,
+                     WNConvTranspose1d, _param_key)
+
+
+# ============================================================================ encoder / decoder
+class Encoder(nn.Module):
+    """models/dac_vrvq.py:19-48. forward(x, return_feat) -> z or (z, feat)."""
+
+    def __init__(self, d_model: int = 64, strides: List[int] = [2, 4, 8, 8], latent_dim: int = 512):
+        super().__init__()
+        blocks = [WNConv1d(1, d_model, kernel_size=7, padding=3)]
+        for stride in strides:
+            d_model *= 2
+            blocks += [EncoderBlock(d_model, stride=stride)]
+        blocks += [Snake1d(d_model), WNConv1d(d_model, latent_dim, kernel_size=3, padding=1)]
+        self.block = nn.Sequential(*blocks)
+
+    def forward(self, x, return_feat: bool = False):
+        n = len(self.block)
+        x = self.block[0](x)
+        for i in range(1, n - 2):
+            x = self.block[i](x)
+        feat = x  # output of block index n-3 (the last EncoderBlock), models/dac_vrvq.py:43-44
+        out = self.block[n - 1](x, snake=self.block[n - 2])
+        return (out, feat) if return_feat else out
+
+
+class Decoder(nn.Module):
+    """models/dac_vrvq.py:51-80: conv k7, DecoderBlocks, Snake, conv k7, Tanh (fused)."""
+
+    def __init__(self, input_channel, channels, rates, d_out: int = 1):
+        super().__init__()
+        layers = [WNConv1d(input_channel, channels, kernel_size=7, padding=3)]
+        output_dim = channels
+        for i, stride in enumerate(rates):
+            input_dim = channels // 2 ** i
+            output_dim = channels // 2 ** (i + 1)
+            layers += [DecoderBlock(input_dim, output_dim, stride)]
+        layers += [Snake1d(output_dim), WNConv1d(output_dim, d_out, kernel_size=7, padding=3),
+                   nn.Tanh()]
+        self.model = nn.Sequential(*layers)
+
+    def forward(self, x):
+        n = len(self.model)
+        x = self.model[0](x)
+        for i in range(1, n - 3):
+            x = self.model[i](x)
+        return self.model[n - 2](x, snake=self.model[n - 3], epilogue=ops.EPI_TANH)
+
+
+# ============================================================================ importance subnet
+class ImportanceSubnet(nn.Module):
+    """models/importance_subnet.py:6-45: [Snake, WN k3 conv] x 6 then Sigmoid (fused)."""
+
+    def __init__(self, d_input, d_feat, intermediate_channels: list = [512, 128, 32, 8],
+                 out_channels=1, detach_input: bool = False):
+        super().__init__()
+        self.in_block = nn.Sequential(Snake1d(d_input),
+                                      WNConv1d(d_input, d_feat, kernel_size=3, padding=1))
+        in_ch = [d_feat] + list(intermediate_channels)
+        out_ch = list(intermediate_channels) + [out_channels]
+        self.blocks = nn.ModuleList([
+            nn.Sequential(Snake1d(in_ch[i]), WNConv1d(in_ch[i], out_ch[i], kernel_size=3, padding=1))
+            for i in range(len(in_ch))
+        ])
+        self.act_fn = nn.Sigmoid()
+        self.detach_input = detach_input  # forward-only here: detach is a no-op
+
+    def forward(self, x_in):
+        x = self.in_block[1](x_in, snake=self.in_block[0])
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            x = blk[1](x, snake=blk[0], epilogue=ops.EPI_SIGMOID if i == last else ops.EPI_NONE)
+        return x  # (B, 1, T) in (0, 1)
+
+
+# ============================================================================ quantizers
+class VectorQuantize(nn.Module):
+    """Factorised, L2-normalised VQ stage (models/quantize.py:21-103)."""
+
+    def __init__(self, input_dim: int, codebook_size: int, codebook_dim: int):
+        super().__init__()
+        self.codebook_size = codebook_size
+        self.codebook_dim = codebook_dim
+        self.in_proj = WNConv1d(input_dim, codebook_dim, kernel_size=1)
+        self.out_proj = WNConv1d(codebook_dim, input_dim, kernel_size=1)
+        self.codebook = nn.Embedding(codebook_size, codebook_dim)
+
+    def forward(self, z, loss_per_frame: bool = False):
+        """Single-stage quantisation (the fused RVQ kernels with nq = 1).
+
+        Returns z_q, commitment_loss, codebook_loss, indices, z_e as the reference does
+        (losses per frame (B, T) if loss_per_frame else per item (B,))."""
+        st = _stack_stages([self], z.device)
+        codes, latents, loss_pf, zst = ops.rvq_codes(z.contiguous(), *st.codes_args())
+        _, z_q, _ = ops.rvq_expand(zst, st.w_out, st.b_out, None, 1.0, want_z_q_is=False,
+                                   want_mask=False)
+        loss = loss_pf[:, 0, :]
+        if not loss_per_frame:
+            loss = loss.mean(1)
+        return z_q, loss, loss.clone(), codes[:, 0, :], latents
+
+
+class _Stacked:
+    """Per-stage RVQ weights folded and stacked in the kernels' layouts."""
+
+    def __init__(self, quantizers, device):
+        w_in_t, b_in, cb, w_out, b_out = [], [], [], [], []
+        for q in quantizers:
+            wi = q.in_proj.folded_weight()                       # (d, D, 1)
+            w_in_t.append(wi.reshape(wi.shape[0], wi.shape[1]).t())
+            b_in.append(q.in_proj.bias.detach())
+            cb.append(q.codebook.weight.detach())
+            wo = q.out_proj.folded_weight()                      # (D, d, 1)
+            w_out.append(wo.reshape(wo.shape[0], wo.shape[1]))
+            b_out.append(q.out_proj.bias.detach())
+        self.w_in_t = torch.stack(w_in_t).contiguous()
+        self.b_in = torch.stack(b_in).contiguous()
+        self.cb = torch.stack(cb).contiguous()
+        self.cbn, self.c2 = ops.codebook_prep(self.cb)
+        self.w_out = torch.stack(w_out).contiguous()
+        self.b_out = torch.stack(b_out).contiguous()
+
+    def codes_args(self):
+        return (self.w_in_t, self.b_in, self.cb, self.cbn, self.c2, self.w_out, self.b_out)
+
+    def prefix(self, n):
+        s = _Stacked.__new__(_Stacked)
+        for k in ("w_in_t", "b_in", "cb", "cbn", "c2", "w_out", "b_out"):
+            setattr(s, k, getattr(self, k)[:n].contiguous())
+        return s
+
+
+def _stack_stages(quantizers, device):
+    return _Stacked(quantizers, device)
+
+
+class ResidualVectorQuantize(nn.Module):
+    """CBR residual VQ (models/quantize.py:106-285)."""
+
+    def __init__(self, input_dim: int = 512, n_codebooks: int = 9, codebook_size: int = 1024,
+                 codebook_dim: Union[int, list] = 8, quantizer_dropout: float = 0.0):
+        super().__init__()
+        if isinstance(codebook_dim, int):
+            codebook_dim = [codebook_dim for _ in range(n_codebooks)]
+        self.n_codebooks = n_codebooks
+        self.codebook_dim = codebook_dim
+        self.codebook_size = codebook_size
+        self.quantizers = nn.ModuleList([
+            VectorQuantize(input_dim, codebook_size, codebook_dim[i]) for i in range(n_codebooks)
+        ])
+        self.quantizer_dropout = quantizer_dropout
+        self._stack_cache = None
+
+    def stacked(self) -> _Stacked:
+        params = []
+        for q in self.quantizers:
+            params += [q.in_proj.weight_g, q.in_proj.weight_v, q.in_proj.bias, q.codebook.weight,
+                       q.out_proj.weight_g, q.out_proj.weight_v, q.out_proj.bias]
+        key = _param_key(*params)
+        if self._stack_cache is None or self._stack_cache[0] != key:
+            self._stack_cache = (key, _Stacked(self.quantizers, params[0].device))
+        return self._stack_cache[1]
+
+    def _check_mode(self):
+        if self.training:
+            raise NotImplementedError(
+                "vrvq_amd implements the inference path; the training-mode quantizer "
+                "(quantizer dropout / random levels, models/quantize.py:175-194, 374-414) is "
+                "the next row of SURVEY.md §8f — call .eval()")
+
+    def forward(self, z, n_quantizers: int = None):
+        self._check_mode()
+        n = self.n_codebooks if n_quantizers is None else min(int(n_quantizers), self.n_codebooks)
+        st = self.stacked()
+        if n < self.n_codebooks:
+            st = st.prefix(n)
+        codes, latents, loss_pf, zst = ops.rvq_codes(z.contiguous(), *st.codes_args())
+        _, z_q, _ = ops.rvq_expand(zst, st.w_out, st.b_out, None, 1.0, want_z_q_is=False,
+                                   want_mask=False)
+        loss = ops.masked_loss(loss_pf, None)  # sum_i mean_{b,t} loss_i (mask all-true in eval)
+        return {"z_q": z_q, "codes": codes, "latents": latents,
+                "commitment_loss": loss, "codebook_loss": loss.clone()}
+
+    def from_codes(self, codes: torch.Tensor, return_z_q_is: bool = False):
+        raise NotImplementedError("from_codes (codes -> audio decode) is SURVEY.md §8f row 2")
+
+    def from_latents(self, latents: torch.Tensor):
+        raise NotImplementedError("from_latents is outside the hot path (SURVEY.md §8f)")
+
+
+class VBRResidualVectorQuantize(ResidualVectorQuantize):
+    """Variable-bitrate RVQ with importance-map gating (models/quantize.py:288-449)."""
+
+    def __init__(self, *, input_dim: int = 512, n_codebooks: int = 9, codebook_size: int = 1024,
+                 codebook_dim: Union[int, list] = 8, quantizer_dropout: float = 0.0,
+                 full_codebook_rate: float = 0.5, level_min: float, level_max: float,
+                 level_dist: str = "uniform", detach_imp_map_input: bool = False,
+                 imp2mask_alpha: float = 1.0):
+        super().__init__(input_dim=input_dim, n_codebooks=n_codebooks, codebook_size=codebook_size,
+                         codebook_dim=codebook_dim, quantizer_dropout=quantizer_dropout)
+        self.full_codebook_rate = full_codebook_rate
+        self.level_min = level_min
+        self.level_max = level_max
+        self.level_dist = level_dist
+        self.detach_imp_map_input = detach_imp_map_input
+        self.imp2mask_alpha = imp2mask_alpha
+        self.imp_subnet = ImportanceSubnet(d_input=input_dim, d_feat=input_dim,
+                                           intermediate_channels=[512, 128, 32, 8], out_channels=1,
+                                           detach_input=detach_imp_map_input)
+
+    def forward(self, z: torch.Tensor, n_quantizers: int = None, feat_enc: torch.Tensor = None,
+                level: float = None, want_z_q_is: bool = True):
+        self._check_mode()
+        B, D, T = z.shape
+        nq = self.n_codebooks
+        if n_quantizers is None:
+            if level is None:
+                raise AssertionError("level must be specified in VBR mode")
+            mode = "VBR"
+        else:
+            mode = "CBR"
+            if int(n_quantizers) < nq:
+                # The reference stacks n_quantizers z_q_i against an (B, Nq, T) mask of ones and
+                # fails with a shape mismatch at models/quantize.py:421.
+                raise RuntimeError(
+                    f"VBRResidualVectorQuantize in CBR mode needs n_quantizers >= n_codebooks "
+                    f"({n_quantizers} < {nq}), as in the reference")
+        st = self.stacked()
+        codes, latents, loss_pf, zst = ops.rvq_codes(z.contiguous(), *st.codes_args())
+        if mode == "VBR":
+            imp_map = self.imp_subnet(feat_enc.contiguous())                 # (B, 1, T)
+            imp = imp_map.reshape(B, T)
+            z_q_is, z_q, mask = ops.rvq_expand(zst, st.w_out, st.b_out, imp, float(level),
+                                               want_z_q_is=want_z_q_is)
+        else:
+            imp_map = None
+            z_q_is, z_q, mask = ops.rvq_expand(zst, st.w_out, st.b_out, None, 1.0,
+                                               want_z_q_is=want_z_q_is)
+        loss = ops.masked_loss(loss_pf, mask)
+        return {
+            "z_q": z_q,
+            "z_q_is": z_q_is,
+            "codes": codes,
+            "latents": latents,
+            "commitment_loss": loss,
+            "codebook_loss": loss.clone(),
+            "imp_map": imp_map,
+            "mask_imp": mask,
+        }
+
+    def from_codes(self, codes: torch.Tensor, return_z_q_is=False):
+        raise NotImplementedError
+
+    def from_latents(self, latents: torch.Tensor):
+        raise NotImplementedError
+
+
+# ============================================================================ codec
+class CodecMixin:
+    """Delay / output-length bookkeeping of models/dac_base.py:61-127."""
+
+    @property
+    def padding(self):
+        if not hasattr(self, "_padding"):
+            self._padding = True
+        return self._padding
+
+    @padding.setter
+    def padding(self, value):
+        if not value:
+            raise NotImplementedError("padding=False windows belong to the chunked compress "
+                                      "path (SURVEY.md §8f row 4)")
+        self._padding = True
+
+    def _conv_layers(self):
+        return [m for m in self.modules() if isinstance(m, (WNConv1d, WNConvTranspose1d))]
+
+    def get_delay(self):
+        l_out = self.get_output_length(0)
+        L = l_out
+        for layer in reversed(self._conv_layers()):
+            d, k, s = layer.dilation[0], layer.kernel_size[0], layer.stride[0]
+            if isinstance(layer, WNConvTranspose1d):
+                L = ((L - d * (k - 1) - 1) / s) + 1
+            else:
+                L = (L - 1) * s + d * (k - 1) + 1
+            L = math.ceil(L)
+        return (L - l_out) // 2
+
+    def get_output_length(self, input_length):
+        L = input_length
+        for layer in self._conv_layers():
+            d, k, s = layer.dilation[0], layer.kernel_size[0], layer.stride[0]
+            if isinstance(layer, WNConv1d):
+                L = ((L - d * (k - 1) - 1) / s) + 1
+            else:
+                L = (L - 1) * s + d * (k - 1) + 1
+            L = math.floor(L)
+        return L
+
+
+class DAC_VRVQ(nn.Module, CodecMixin):
+    """Drop-in for models/dac_vrvq.py:83-252 (`DAC_VRVQ`)."""
+
+    def __init__(self, encoder_dim: int = 64, encoder_rates: List[int] = [2, 4, 8, 8],
+                 latent_dim: int = None, decoder_dim: int = 1536,
+                 decoder_rates: List[int] = [8, 8, 4, 2], n_codebooks: int = 9,
+                 codebook_size: Union[int, list] = 1024, codebook_dim: Union[int, list] = 8,
+                 quantizer_dropout: float = 0.0, sample_rate: int = 44100,
+                 model_type: str = "VBR", full_codebook_rate: float = 0.0,
+                 level_min: float = None, level_max: float = None, level_dist: str = "uniform",
+                 detach_imp_map_input: bool = False, imp2mask_alpha: float = 1.0):
+        super().__init__()
+        self.encoder_dim = encoder_dim
+        self.encoder_rates = encoder_rates
+        self.decoder_dim = decoder_dim
+        self.decoder_rates = decoder_rates
+        self.sample_rate = sample_rate
+        if latent_dim is None:
+            latent_dim = encoder_dim * (2 ** len(encoder_rates))
+        self.latent_dim = latent_dim
+        self.hop_length = int(np.prod(encoder_rates))
+        self.encoder = Encoder(encoder_dim, encoder_rates, latent_dim)
+        self.n_codebooks = n_codebooks
+        self.codebook_size = codebook_size
+        self.codebook_dim = codebook_dim
+        self.model_type = model_type
+        if model_type == "CBR":
+            self.quantizer = ResidualVectorQuantize(input_dim=latent_dim, n_codebooks=n_codebooks,
+                                                    codebook_size=codebook_size,
+                                                    codebook_dim=codebook_dim,
+                                                    quantizer_dropout=quantizer_dropout)
+        elif model_type == "VBR":
+            self.quantizer = VBRResidualVectorQuantize(
+                input_dim=latent_dim, n_codebooks=n_codebooks, codebook_size=codebook_size,
+                codebook_dim=codebook_dim, quantizer_dropout=quantizer_dropout,
+                full_codebook_rate=full_codebook_rate, level_min=level_min, level_max=level_max,
+                level_dist=level_dist, detach_imp_map_input=detach_imp_map_input,
+                imp2mask_alpha=imp2mask_alpha)
+        else:
+            raise ValueError(f"Invalid RVQ model_type: {model_type}")
+        self.decoder = Decoder(latent_dim, decoder_dim, decoder_rates)
+        self.delay = self.get_delay()
+
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    def preprocess(self, audio_data, sample_rate):
+        """Right-pad to a multiple of hop_length (models/dac_vrvq.py:164-173)."""
+        if sample_rate is None:
+            sample_rate = self.sample_rate
+        assert sample_rate == self.sample_rate
+        length = audio_data.shape[-1]
+        right_pad = math.ceil(length / self.hop_length) * self.hop_length - length
+        return nn.functional.pad(audio_data, (0, right_pad))
+
+    def encode(self, audio_data: torch.Tensor, n_quantizers: int = None, level: int = 1,
+               want_z_q_is: bool = True):
+        """models/dac_vrvq.py:176-213. Returns the quantizer's output dict.
+
+        `want_z_q_is=False` skips materialising the (B, Nq, D, T) per-codebook tensor when the
+        caller does not need it (it is ~90 % of the quantizer's HBM traffic); the default keeps
+        the reference's dict."""
+        z, feat = self.encoder(audio_data.contiguous(), return_feat=True)
+        if self.model_type == "CBR":
+            return self.quantizer(z, n_quantizers)
+        return self.quantizer(z, n_quantizers, feat, level, want_z_q_is=want_z_q_is)
+
+    def decode(self, z: torch.Tensor):
+        """models/dac_vrvq.py:215-220."""
+        return self.decoder(z.contiguous())
+
+    def forward(self, audio_data: torch.Tensor, sample_rate: int = None, n_quantizers: int = None,
+                level: int = 1):
+        """models/dac_vrvq.py:222-252."""
+        length = audio_data.shape[-1]
+        audio_data = self.preprocess(audio_data, sample_rate)
+        out = self.encode(audio_data, n_quantizers, level) if self.model_type == "VBR" \
+            else self.encode(audio_data, n_quantizers)
+        z_q = out["z_q"]
+        x = self.decode(z_q)
+        return {
+            "audio": x[..., :length],
+            "z": z_q,
+            "codes": out["codes"],
+            "latents": out["latents"],
+            "vq/commitment_loss": out["commitment_loss"],
+            "vq/codebook_loss": out["codebook_loss"],
+            "imp_map": out.get("imp_map", None),
+            "mask_imp": out.get("mask_imp", None),
+        }

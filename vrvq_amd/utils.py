@@ -1,0 +1,77 @@
+"""Importance-map gating and rate helpers (reference: models/utils.py:45-73,
+scripts/inference.py:88-112) on gfx950 kernels."""
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import torch
+
+from . import ops
+
+
+def _as_scaled(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype != torch.float32:
+        raise RuntimeError("importance map must be float32")
+    return x.contiguous()
+
+
+def generate_mask_hard(x: torch.Tensor, nq: int) -> torch.Tensor:
+    """mask[b, n, t] = 1.0 if x[b, 0, t] - n >= 0 else 0.0   (models/utils.py:55-61)."""
+    return ops.mask_hard(_as_scaled(x), nq)
+
+
+def generate_mask_ste(x: torch.Tensor, nq: int, alpha: float = 1) -> torch.Tensor:
+    """Forward value of the straight-through mask (models/utils.py:45-53).
+
+    mask_smooth + (mask_quant - mask_smooth).detach() equals the hard mask exactly in fp32
+    (for q = 0 it is s + (-s) = 0; for q = 1, s >= 0.5 and 1 - s is exact by Sterbenz), so the
+    forward pass is the hard-mask kernel; the log-cosh backward belongs to the training row."""
+    return ops.mask_hard(_as_scaled(x), nq)
+
+
+def scale_importance(imp_map: torch.Tensor, a: float, c: float = 1.0) -> torch.Tensor:
+    """(imp_map * a) * c with fp32 roundings (see include/vrvq.h vrvq_scale_imp)."""
+    return ops.scale_imp(_as_scaled(imp_map), a, c)
+
+
+def cal_bpf_from_mask(mask: torch.Tensor, bits_per_codebook: Sequence[float]) -> float:
+    """Bits per frame: sum(mask * bits[n]) / (B * T), returned as a Python float like the
+    reference's `.item()` (models/utils.py:64-73)."""
+    return float(cal_bpf_tensor(mask, bits_per_codebook).item())
+
+
+def cal_bpf_tensor(mask: torch.Tensor, bits_per_codebook: Sequence[float]) -> torch.Tensor:
+    """Same as cal_bpf_from_mask but returns a 0-d device tensor (no host sync)."""
+    bits = torch.as_tensor(list(bits_per_codebook), dtype=torch.float32).to(mask.device)
+    return ops.bpf(mask.contiguous(), bits)
+
+
+def masked_sum(z_q_is: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """z_q = sum_i z_q_is[:, i] * mask[:, i, None, :]   (scripts/inference.py:99-100)."""
+    return ops.masked_sum(z_q_is.contiguous(), mask.contiguous())
+
+
+def level_sweep(model, audio: torch.Tensor, levels: Sequence[float], bits_per_codebook: int = 10,
+                decode: bool = True):
+    """The reference's VBR level sweep (scripts/inference.py:88-112) without file I/O.
+
+    Encodes once (level 1), then for each level: hard mask of imp_map * (level * Nq),
+    masked sum of z_q_is, decode, bpf and kbps. Returns a list of dicts."""
+    n_q = model.n_codebooks
+    with torch.no_grad():
+        x = model.preprocess(audio, model.sample_rate)
+        enc = model.encode(x, n_quantizers=None, level=1)
+    imp_map = enc["imp_map"]
+    out = []
+    for level in levels:
+        level_scaled = level * n_q
+        s = scale_importance(imp_map, level_scaled, 1.0)
+        mask = generate_mask_hard(s, n_q)
+        z_q = masked_sum(enc["z_q_is"], mask)
+        recon = model.decode(z_q) if decode else None
+        bpf = cal_bpf_from_mask(mask, [bits_per_codebook] * n_q)
+        kbps = bpf * math.floor(model.sample_rate / model.hop_length) / 1000
+        out.append({"level": level, "level_scaled": level_scaled, "mask": mask, "z_q": z_q,
+                    "recon": recon, "bpf": bpf, "kbps": kbps})
+    return out
