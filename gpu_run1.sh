@@ -1,0 +1,14 @@
+#!/bin/bash
+# step runner: stop at the first GPU fault/abort/timeout; tolerate pytest assertion failures (rc 1)
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+run() { # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name" ; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
+  echo "=== $name rc=$rc"; tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+run bench 600 python bench.py --steps 10 --warmup 3
