@@ -39,6 +39,10 @@ enum vrvq_epilogue_t { VRVQ_EPI_NONE = 0, VRVQ_EPI_TANH = 1, VRVQ_EPI_SIGMOID = 
 const char* vrvq_status_string(int status);
 /* Library version (major*10000 + minor*100 + patch). */
 int vrvq_version(void);
+/* Diagnostics: in a library built with -DVRVQ_STAMPS, vrvq_rvq_codes writes per-workgroup,
+ * per-stage s_memtime stamps ([blocks][nq][8] uint64) into buf (NULL disables). A no-op in
+ * the product build. */
+int vrvq_debug_set_stamps(unsigned long long* buf);
 
 /* ---------------------------------------------------------------------------------------
  * Weight preparation (once per load_state_dict; the reference recomputes weight norm on

@@ -10,7 +10,7 @@ import os
 import threading
 
 LIB_NAME = "libvrvq_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("VRVQ_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -34,7 +34,8 @@ SIGNATURES = {
     "vrvq_masked_sum": [_P, _P, _I, _I, _I, _I, _P, _P],
     "vrvq_bpf": [_P, _P, _I, _I, _I, _P, _P],
 }
-EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)}
+EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
+         "vrvq_debug_set_stamps": ([_P], _I)}
 
 _lock = threading.Lock()
 _lib = None

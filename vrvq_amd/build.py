@@ -13,8 +13,10 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvrvq_hip.so")
 ARCH = os.environ.get("VRVQ_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}",
-         "-Wall", "-Wno-unused-function"]
+# -fno-slp-vectorize: the SLP pass packs independent fp32 chains into v_pk_* with extra
+# v_mov shuffles and +40 VGPRs in the RVQ kernel; packed math is written explicitly instead.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
+         f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 
 def sources():
@@ -52,5 +54,18 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+def build_stamped(verbose: bool = True) -> str:
+    """Diagnostic build with in-kernel s_memtime stamps (tools/rvq_stamps.py)."""
+    out = os.path.join(HERE, "libvrvq_hip_stamps.so")
+    cmd = [hipcc()] + FLAGS + ["-DVRVQ_STAMPS", "-I", os.path.join(REPO, "include"), "-o", out] + sources()
+    if verbose:
+        print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 if __name__ == "__main__":
-    build_library(force="--force" in sys.argv)
+    if "--stamps" in sys.argv:
+        build_stamped()
+    else:
+        build_library(force="--force" in sys.argv)

@@ -153,32 +153,138 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   }
 
   // ---- epilogue: bias, residual, activation, store ----
+  // Per accumulator tile: every load (bias, residual) is issued before any store, so the
+  // 16 round trips overlap instead of serialising behind possibly-aliasing stores.
+  if (a.up == 0) {
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = n0 + wn * TN + j * 32 + lr;
+    for (int i = 0; i < RM; ++i) {
+      const int mb = m0 + wm * TM + i * 32 + 4 * lh;
+      float bv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= a.M || n >= a.ng) continue;
-        int co, t;
-        if (a.up == 0) {
-          co = m;
-          t = n;
-        } else {
-          co = m / a.up;
-          t = n * a.up + (m - co * a.up) - a.up_pad;
-          if (t < 0 || t >= a.ylen) continue;
+        const int m = mb + (r & 3) + 8 * (r >> 2);
+        bv[r] = (a.bias && m < a.M) ? a.bias[m] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = n0 + wn * TN + j * 32 + lr;
+        const size_t ob = ((size_t)b * a.cout + mb) * a.ylen + n;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r] + bv[r];
+        if (a.res) {
+          float rv[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mo = (r & 3) + 8 * (r >> 2);
+            rv[r] = (mb + mo < a.M && n < a.ng) ? a.res[ob + (size_t)mo * a.ylen] : 0.0f;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = rv[r] + v[r];
         }
-        float v = acc[i][j][r];
-        if (a.bias) v = v + a.bias[co];
-        const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mo = (r & 3) + 8 * (r >> 2);
+          if (mb + mo < a.M && n < a.ng) a.y[ob + (size_t)mo * a.ylen] = apply_epi(v[r], a.epi);
+        }
+      }
+    }
+  } else {
+    // transposed conv: GEMM row m = co*up + phase, output t = n*up + phase - up_pad
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int mb = m0 + wm * TM + i * 32 + 4 * lh;
+      int cor[16], phr[16];
+      float bv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + (r & 3) + 8 * (r >> 2);
+        const int co = m / a.up;
+        cor[r] = m < a.M ? co : -1;
+        phr[r] = m - co * a.up - a.up_pad;
+        bv[r] = (a.bias && m < a.M) ? a.bias[co] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = n0 + wn * TN + j * 32 + lr;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int t = n * a.up + phr[r];
+          if (cor[r] >= 0 && n < a.ng && t >= 0 && t < a.ylen)
+            a.y[((size_t)b * a.cout + cor[r]) * a.ylen + t] = acc[i][j][r] + bv[r];
+        }
+      }
+    }
+  }
+}
+
+// Small-Cout conv (Cout <= 8, stride 1): the decoder's 96->1 k7 + Tanh output layer and the
+// importance subnet's 32->8 / 8->1 k3 tail. An MFMA tile would be >= 75 % padding and the layer
+// is HBM-bound on reading x, so: one thread per output sample, snake(x) rows of SC channels
+// staged in LDS per step (window 256 + (k-1)*dil), every output channel accumulated in VGPRs.
+constexpr int SMALL_BT = 256;
+constexpr int SMALL_SC = 16;
+constexpr int SMALL_COUT = 8;
+
+__global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [SMALL_SC][XW]
+  const int XW = SMALL_BT + (ks - 1) * a.dil;
+  const int n_t = (a.ng + SMALL_BT - 1) / SMALL_BT;
+  const int b = blockIdx.x / n_t;
+  const int t0 = (blockIdx.x - b * n_t) * SMALL_BT;
+  const int tid = threadIdx.x;
+  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  float acc[SMALL_COUT];
+#pragma unroll
+  for (int c = 0; c < SMALL_COUT; ++c) acc[c] = 0.0f;
+
+  for (int ci0 = 0; ci0 < a.cin; ci0 += SMALL_SC) {
+    const int nc = min(SMALL_SC, a.cin - ci0);
+    for (int e = tid; e < nc * XW; e += 256) {
+      const int cl = e / XW, p = e - cl * XW;
+      const int ci = ci0 + cl;
+      const int t = t0 - a.pad + p;
+      float v = 0.0f;
+      if (t >= 0 && t < a.tin) {
+        v = xb[(size_t)ci * a.tin + t];
+        if (a.alpha) v = snake_act(v, a.alpha[ci], a.inv_alpha[ci]);
+      }
+      xs[cl * XW + p] = v;
+    }
+    __syncthreads();
+    for (int cl = 0; cl < nc; ++cl) {
+      const float* wr = a.w + (size_t)(ci0 + cl) * ks * a.m_pad;
+      for (int k = 0; k < ks; ++k) {
+        const float xv = xs[cl * XW + tid + k * a.dil];
+#pragma unroll
+        for (int c = 0; c < SMALL_COUT; ++c)
+          if (c < a.M) acc[c] = fmaf(wr[k * a.m_pad + c], xv, acc[c]);
+      }
+    }
+    __syncthreads();
+  }
+  const int t = t0 + tid;
+  if (t < a.ng) {
+#pragma unroll
+    for (int c = 0; c < SMALL_COUT; ++c) {
+      if (c < a.M) {
+        float v = acc[c];
+        if (a.bias) v = v + a.bias[c];
+        const size_t o = ((size_t)b * a.cout + c) * a.ylen + t;
         if (a.res) v = a.res[o] + v;
         a.y[o] = apply_epi(v, a.epi);
       }
     }
   }
+}
+
+int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
+  const size_t lds = (size_t)SMALL_SC * (SMALL_BT + (ks - 1) * a.dil) * sizeof(float);
+  if (lds > 64 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  const long long nblk = (long long)batch * ((a.ng + SMALL_BT - 1) / SMALL_BT);
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  hipLaunchKernelGGL(conv_small_cout_kernel, dim3((unsigned)nblk), dim3(256), lds, st, a, ks);
+  return vrvq_launch_status();
 }
 
 template <int BM, int BN, int WM, int KS>
@@ -294,6 +400,7 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
   a.stride = stride; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0;
   a.ylen = tout; a.epi = epilogue;
+  if (cout <= SMALL_COUT && stride == 1) return launch_small(a, batch, k, as_stream(stream));
   return dispatch_ks(k, a, batch, as_stream(stream));
 }
 
