@@ -146,6 +146,12 @@ CONV_CASES = [
     (1, 1024, 1536, 87, 7, 1, 3, 1, False, False, 0),
     (1, 768, 768, 5, 7, 1, 3, 1, True, True, 0),
     (1, 16, 16, 1, 7, 1, 3, 1, True, False, 0),
+    (1, 192, 192, 600, 7, 1, 9, 3, True, False, 0),
+    (1, 192, 192, 300, 1, 1, 0, 1, True, True, 0),
+    (1, 96, 96, 300, 1, 1, 0, 1, True, True, 0),
+    (2, 768, 768, 100, 7, 1, 27, 9, True, False, 0),
+    (2, 512, 512, 96, 7, 1, 3, 1, True, False, 0),
+    (1, 96, 8, 500, 7, 1, 3, 1, True, True, 2),
 ]
 
 

@@ -1,0 +1,66 @@
+#!/usr/bin/env python
+"""Single-layer micro-bench of the conv kernels (HIP events; use under rocprofv3 for PMC).
+
+    python tools/conv_bench.py --cin 384 --cout 384 --t 5568 --k 7 --dil 3 --batch 32
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from vrvq_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cin", type=int, default=384)
+    ap.add_argument("--cout", type=int, default=384)
+    ap.add_argument("--t", type=int, default=5568)
+    ap.add_argument("--k", type=int, default=7)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--dil", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--res", action="store_true")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--convt", type=int, default=0, help="transposed conv with this stride")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(0)
+    x = (torch.rand(args.batch, args.cin, args.t, generator=g) - 0.5).to(dev)
+    alpha = (torch.rand(args.cin, generator=g) + 0.5).to(dev)
+    inv = ops.snake_inv_alpha(alpha)
+    if args.convt:
+        w = (torch.randn(args.cin, args.cout, 2 * args.convt, generator=g) * 0.02).to(dev)
+        wp, cp = ops.pack_convt1d_weight(w, args.convt)
+        b = torch.zeros(args.cout, device=dev)
+        fn = lambda: ops.conv_transpose1d(x, wp, args.cout, cp, args.convt, b, alpha, inv)
+        flops = 2.0 * args.batch * args.cin * args.cout * 2 * args.convt * args.t
+    else:
+        w = (torch.randn(args.cout, args.cin, args.k, generator=g) * 0.02).to(dev)
+        wp, cp = ops.pack_conv1d_weight(w)
+        b = torch.zeros(args.cout, device=dev)
+        pad = (args.k - 1) * args.dil // 2 if args.stride == 1 else (args.stride + 1) // 2
+        tout = (args.t + 2 * pad - args.dil * (args.k - 1) - 1) // args.stride + 1
+        res = torch.randn(args.batch, args.cout, tout, device=dev) if args.res else None
+        fn = lambda: ops.conv1d(x, wp, args.cout, cp, args.k, args.stride, pad, args.dil, b, alpha,
+                                inv, res)
+        flops = 2.0 * args.batch * args.cin * args.cout * args.k * tout
+    for _ in range(3):
+        fn()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(args.iters):
+        ev[0].record()
+        fn()
+        ev[1].record()
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    ts.sort()
+    med = ts[len(ts) // 2]
+    print(f"{vars(args)}: median {med*1e3:.1f} us, {flops / med / 1e9:.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()

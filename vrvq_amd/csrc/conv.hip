@@ -33,6 +33,7 @@ struct ConvArgs {
   int m_pad;
   int cout;
   int stride, pad, dil;
+  int ssh;                 // log2(stride) for a power-of-two stride >= 2 (phase-split window), else 0
   int ng;                  // GEMM columns (output positions of the GEMM)
   int up, up_pad;          // transposed conv: upsample factor and its padding (0 = normal)
   int ylen;                // output row length
@@ -40,10 +41,12 @@ struct ConvArgs {
   int n_mt, n_nt;          // M tiles, N tiles
 };
 
-template <int KS>
+template <int KS, int BM>
 struct ChunkCfg {
-  // Input channels per K-chunk: keep CK*KS ~ 32..64 rows of W per stage.
-  static constexpr int CK = KS == 1 ? 32 : KS <= 4 ? 16 : KS <= 8 ? 8 : 4;
+  // Input channels per K-chunk: CK*KS ~ 32..64 rows of W per stage (half for 192-row tiles,
+  // so two double-buffered stages still fit twice per CU).
+  static constexpr int CK0 = KS == 1 ? 32 : KS <= 4 ? 16 : KS <= 8 ? 8 : 4;
+  static constexpr int CK = (BM > 128 && CK0 >= 8) ? CK0 / 2 : CK0;
 };
 
 __device__ __forceinline__ float apply_epi(float v, int epi) {
@@ -52,6 +55,16 @@ __device__ __forceinline__ float apply_epi(float v, int epi) {
   return v;
 }
 
+// Largest input window a thread stages per K-chunk: stride <= KS/2 for the strided (k = 2s)
+// encoder convs, dilation <= 9 for the k = 7 residual-unit convs.
+template <int KS, int BN>
+struct WinCfg {
+  static constexpr int SMAX = (KS == 4 || KS == 8 || KS == 16) ? KS / 2 : 1;
+  static constexpr int DMAX = KS == 7 ? 9 : 1;
+  static constexpr int XW_MAX = (BN - 1) * SMAX + (KS - 1) * DMAX + 1;
+  static constexpr int PER_ROW = (XW_MAX + 63) / 64;  // positions per lane per row
+};
+
 template <int BM, int BN, int WM, int KS>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
@@ -59,16 +72,25 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   constexpr int TN = BN / WN;
   constexpr int RM = TM / 32;
   constexpr int RN = TN / 32;
-  constexpr int CK = ChunkCfg<KS>::CK;
+  constexpr int CK = ChunkCfg<KS, BM>::CK;
   constexpr int KROWS = CK * KS;
+  constexpr int WQ4 = KROWS * BM / 4;               // float4 of W per chunk
+  constexpr int WQ = (WQ4 + 255) / 256;             // ... per thread
+  constexpr int XROWS = CK / 4;                     // x rows per wave per chunk
+  constexpr int XPR = WinCfg<KS, BN>::PER_ROW;
   static_assert(RM >= 1 && RN >= 1 && TM % 32 == 0 && TN % 32 == 0, "tile");
-  static_assert(CK % 2 == 0, "CK even");
+  static_assert(CK % 4 == 0, "chunk shape");
 
+  // Two LDS stages: [W chunk | x window] x 2. The next chunk is prefetched into registers
+  // while the current one feeds the MFMAs, then written (with Snake) to the other stage:
+  // one barrier per K-chunk.
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* ws = smem;                 // [KROWS][BM]
-  float* xs = smem + KROWS * BM;    // [CK][XWP]
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
-  const int XWP = (XW + 3) & ~3;
+  // Strided convs store the window phase-split, [phase][position / stride], so the B-operand
+  // read of every tap is unit-stride across lanes (no LDS bank conflicts).
+  const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
+  const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
+  const int STG = KROWS * BM + CK * XWP;
 
   int bid = blockIdx.x;
   const int mt = bid % a.n_mt;
@@ -97,39 +119,66 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const float* xb = a.x + (size_t)b * a.cin * a.tin;
   const int xbase = n0 * a.stride - a.pad;
 
-  for (int ci0 = 0; ci0 < a.cin; ci0 += CK) {
-    // ---- stage W chunk: rows (ci0*KS .. ci0*KS+KROWS) x cols [m0, m0+BM), float4 ----
-    for (int i = tid; i < KROWS * (BM / 4); i += 256) {
-      const int rr = i / (BM / 4);
-      const int cc = (i - rr * (BM / 4)) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ci0 + rr / KS < a.cin)
-        v = *reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc);
-      *reinterpret_cast<float4*>(ws + rr * BM + cc) = v;
-    }
-    // ---- stage snake(x) window: CK rows x XW positions (zero outside [0, tin)) ----
-    for (int cl = wave; cl < CK; cl += 4) {
-      const int ci = ci0 + cl;
-      const bool cvalid = ci < a.cin;
-      float al = 0.f, ia = 0.f;
-      const bool sn = cvalid && a.alpha != nullptr;
-      if (sn) {
-        al = a.alpha[ci];
-        ia = a.inv_alpha[ci];
-      }
-      const float* xr = xb + (size_t)(cvalid ? ci : 0) * a.tin;
-      for (int p = lane; p < XWP; p += 64) {
-        const int t = xbase + p;
-        float v = 0.f;
-        if (cvalid && p < XW && t >= 0 && t < a.tin) {
-          v = xr[t];
-          if (sn) v = snake_act(v, al, ia);
-        }
-        xs[cl * XWP + p] = v;
-      }
-    }
-    __syncthreads();
+  float4 wreg[WQ];
+  float xreg[XROWS][XPR];
 
+  auto load_chunk = [&](int ci0) {
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int idx = tid + q * 256;
+      const int rr = idx / (BM / 4);
+      const int cc = (idx - rr * (BM / 4)) * 4;
+      wreg[q] = (idx < WQ4 && ci0 + rr / KS < a.cin)
+                    ? *reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int rw = 0; rw < XROWS; ++rw) {
+      const int ci = ci0 + wave + 4 * rw;
+      const float* xr = xb + (size_t)ci * a.tin;
+#pragma unroll
+      for (int u = 0; u < XPR; ++u) {
+        const int p = lane + 64 * u;
+        const int t = xbase + p;
+        xreg[rw][u] = (ci < a.cin && p < XW && t >= 0 && t < a.tin) ? xr[t] : 0.0f;
+      }
+    }
+  };
+  auto store_chunk = [&](float* stg, int ci0) {
+    float* ws = stg;
+    float* xs = stg + KROWS * BM;
+#pragma unroll
+    for (int q = 0; q < WQ; ++q)
+      if (tid + q * 256 < WQ4) reinterpret_cast<float4*>(ws)[tid + q * 256] = wreg[q];
+#pragma unroll
+    for (int rw = 0; rw < XROWS; ++rw) {
+      const int cl = wave + 4 * rw;
+      const int ci = ci0 + cl;
+      const bool sn = a.alpha != nullptr && ci < a.cin;
+      const float al = sn ? a.alpha[ci] : 0.f, ia = sn ? a.inv_alpha[ci] : 0.f;
+#pragma unroll
+      for (int u = 0; u < XPR; ++u) {
+        const int p = lane + 64 * u;
+        float v = xreg[rw][u];
+        if (sn) v = snake_act(v, al, ia);  // snake(0) = 0: zero padding commutes with Snake
+        if (a.ssh) {
+          if (p < XW) xs[cl * XWP + (p & (a.stride - 1)) * XP + (p >> a.ssh)] = v;
+        } else if (p < XWP) {
+          xs[cl * XWP + p] = v;
+        }
+      }
+    }
+  };
+
+  int cur = 0;
+  load_chunk(0);
+  store_chunk(smem, 0);
+  __syncthreads();
+  for (int ci0 = 0; ci0 < a.cin; ci0 += CK) {
+    const bool more = ci0 + CK < a.cin;
+    if (more) load_chunk(ci0 + CK);  // global loads in flight during the MFMAs below
+    const float* ws = smem + cur * STG;
+    const float* xs = ws + KROWS * BM;
     // ---- MFMA over the chunk: K order = (tap, channel pair) ----
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -139,9 +188,11 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         float av[RM], bv[RN];
 #pragma unroll
         for (int i = 0; i < RM; ++i) av[i] = ws[(kr * KS + k) * BM + wm * TM + i * 32 + lr];
+        const int col = wn * TN + lr;
+        const int xo = a.ssh ? kr * XWP + (k & (a.stride - 1)) * XP + col + (k >> a.ssh)
+                             : kr * XWP + col + k * a.dil;
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          bv[j] = xs[kr * XWP + (wn * TN + j * 32 + lr) * a.stride + k * a.dil];
+        for (int j = 0; j < RN; ++j) bv[j] = xs[xo + j * 32];
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -149,7 +200,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (more) store_chunk(smem + (cur ^ 1) * STG, ci0 + CK);
     __syncthreads();
+    cur ^= 1;
   }
 
   // ---- epilogue: bias, residual, activation, store ----
@@ -225,18 +278,26 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 constexpr int SMALL_BT = 256;
 constexpr int SMALL_SC = 16;
 constexpr int SMALL_COUT = 8;
+constexpr int SMALL_WMAX = 2048;  // cin * k * cout weights staged in LDS
 
+template <int COUT>
 __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks) {
-  extern __shared__ __attribute__((aligned(16))) float xs[];  // [SMALL_SC][XW]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* w_s = sm;                      // [cin][k][COUT]
+  float* xs = sm + SMALL_WMAX;          // [SMALL_SC][XW]
   const int XW = SMALL_BT + (ks - 1) * a.dil;
   const int n_t = (a.ng + SMALL_BT - 1) / SMALL_BT;
   const int b = blockIdx.x / n_t;
   const int t0 = (blockIdx.x - b * n_t) * SMALL_BT;
   const int tid = threadIdx.x;
   const float* xb = a.x + (size_t)b * a.cin * a.tin;
-  float acc[SMALL_COUT];
+  for (int e = tid; e < a.cin * ks * COUT; e += 256) {
+    const int c = e % COUT, rk = e / COUT;
+    w_s[e] = a.w[(size_t)rk * a.m_pad + c];
+  }
+  float acc[COUT];
 #pragma unroll
-  for (int c = 0; c < SMALL_COUT; ++c) acc[c] = 0.0f;
+  for (int c = 0; c < COUT; ++c) acc[c] = 0.0f;
 
   for (int ci0 = 0; ci0 < a.cin; ci0 += SMALL_SC) {
     const int nc = min(SMALL_SC, a.cin - ci0);
@@ -253,12 +314,12 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
     }
     __syncthreads();
     for (int cl = 0; cl < nc; ++cl) {
-      const float* wr = a.w + (size_t)(ci0 + cl) * ks * a.m_pad;
+      const float* wr = w_s + (size_t)(ci0 + cl) * ks * COUT;
+      const float* xr = xs + cl * XW + tid;
       for (int k = 0; k < ks; ++k) {
-        const float xv = xs[cl * XW + tid + k * a.dil];
+        const float xv = xr[k * a.dil];
 #pragma unroll
-        for (int c = 0; c < SMALL_COUT; ++c)
-          if (c < a.M) acc[c] = fmaf(wr[k * a.m_pad + c], xv, acc[c]);
+        for (int c = 0; c < COUT; ++c) acc[c] = fmaf(wr[k * COUT + c], xv, acc[c]);
       }
     }
     __syncthreads();
@@ -266,7 +327,7 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
   const int t = t0 + tid;
   if (t < a.ng) {
 #pragma unroll
-    for (int c = 0; c < SMALL_COUT; ++c) {
+    for (int c = 0; c < COUT; ++c) {
       if (c < a.M) {
         float v = acc[c];
         if (a.bias) v = v + a.bias[c];
@@ -279,11 +340,15 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
 }
 
 int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
-  const size_t lds = (size_t)SMALL_SC * (SMALL_BT + (ks - 1) * a.dil) * sizeof(float);
+  if (a.cin * ks * (a.M == 1 ? 1 : SMALL_COUT) > SMALL_WMAX) return VRVQ_ERR_UNSUPPORTED;
+  const size_t lds = (size_t)(SMALL_WMAX + SMALL_SC * (SMALL_BT + (ks - 1) * a.dil)) * sizeof(float);
   if (lds > 64 * 1024) return VRVQ_ERR_UNSUPPORTED;
   const long long nblk = (long long)batch * ((a.ng + SMALL_BT - 1) / SMALL_BT);
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-  hipLaunchKernelGGL(conv_small_cout_kernel, dim3((unsigned)nblk), dim3(256), lds, st, a, ks);
+  if (a.M == 1)
+    hipLaunchKernelGGL(conv_small_cout_kernel<1>, dim3((unsigned)nblk), dim3(256), lds, st, a, ks);
+  else
+    hipLaunchKernelGGL(conv_small_cout_kernel<SMALL_COUT>, dim3((unsigned)nblk), dim3(256), lds, st, a, ks);
   return vrvq_launch_status();
 }
 
@@ -293,10 +358,12 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   a.n_mt = (a.M + BM - 1) / BM;
   a.n_nt = (a.ng + BN - 1) / BN;
   if (a.m_pad < a.n_mt * BM) return VRVQ_ERR_ARG;
-  constexpr int CK = ChunkCfg<KS>::CK;
+  constexpr int CK = ChunkCfg<KS, BM>::CK;
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
-  const int XWP = (XW + 3) & ~3;
-  const size_t lds = (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
+  const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
+  const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
+  if (XW > 64 * WinCfg<KS, BN>::PER_ROW) return VRVQ_ERR_UNSUPPORTED;  // window > staged lanes
+  const size_t lds = 2 * (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
   if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, KS>,
@@ -316,18 +383,24 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   auto waste = [&](int bn) { return ((a.ng + bn - 1) / bn) * bn - a.ng; };
   int bn;
   if (a.ng <= 32) bn = 32;
-  else {
-    bn = 128;
-    // Prefer a narrower tile only if it removes a clearly larger share of padding.
-    if (waste(64) * 10 < waste(128) * 7 && a.ng < 4096) bn = 64;
-    if (a.ng <= 128 && waste(32) * 10 < waste(bn) * 7) bn = 32;
+  else if (a.ng <= 96) {
+    // T = 87 / 88 layers: one 96-wide tile per clip when that still gives >= 1.5 workgroups
+    // per CU, otherwise three 32-wide tiles (more workgroups for the deep-K, narrow-N GEMMs).
+    const long long blocks96 = (long long)((a.M + 127) / 128) * batch;
+    bn = blocks96 >= 384 ? 96 : 32;
   }
+  else if (a.ng < 4096 && waste(64) * 10 < waste(128) * 7) bn = 64;
+  else bn = 128;
   if (a.M <= 32) return launch_cfg<32, 128, 1, KS>(a, batch, st);
   if (bn == 32) return launch_cfg<128, 32, 4, KS>(a, batch, st);
+  if (bn == 96) return launch_cfg<128, 96, 4, KS>(a, batch, st);
   if (a.M <= 64) {
     if (bn == 64) return launch_cfg<64, 64, 2, KS>(a, batch, st);
     return launch_cfg<64, 128, 2, KS>(a, batch, st);
   }
+  // 96- and 192-row tiles: no padded rows for the C = 96 / 192 decoder blocks
+  if (a.M <= 96) return launch_cfg<96, 128, 1, KS>(a, batch, st);
+  if (KS >= 3 && a.M % 128 != 0 && a.M % 192 == 0) return launch_cfg<192, 128, 2, KS>(a, batch, st);
   if (bn == 64) return launch_cfg<128, 64, 2, KS>(a, batch, st);
   return launch_cfg<128, 128, 2, KS>(a, batch, st);
 }
@@ -399,8 +472,12 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   a.res = residual; a.y = y;
   a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
   a.stride = stride; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0;
+  a.ssh = 0;
+  if (stride > 1 && (stride & (stride - 1)) == 0)
+    while ((1 << a.ssh) < stride) ++a.ssh;
   a.ylen = tout; a.epi = epilogue;
-  if (cout <= SMALL_COUT && stride == 1) return launch_small(a, batch, k, as_stream(stream));
+  if (cout <= SMALL_COUT && stride == 1 && cin * k * (cout == 1 ? 1 : SMALL_COUT) <= SMALL_WMAX)
+    return launch_small(a, batch, k, as_stream(stream));
   return dispatch_ks(k, a, batch, as_stream(stream));
 }
 
