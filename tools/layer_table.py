@@ -1,0 +1,92 @@
+#!/usr/bin/env python
+"""Per-layer conv efficiency from a rocprofv3 kernel trace.
+
+Runs the model's forward on CPU with the ops layer replaced by shape-only fakes to get the
+conv launch sequence (Cin, Cout, k, stride, dil, Tout), then matches it against the last step's
+conv dispatches in a rocprofv3 --kernel-trace CSV and prints FLOPs, time and TFLOP/s per layer.
+
+    python tools/layer_table.py gpurun_out/prof_X/run_kernel_trace.csv [--batch 32]
+"""
+import argparse
+import csv
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vrvq_amd import ops  # noqa: E402
+
+CALLS = []
+
+
+def _fake():
+    def conv1d(x, wp, cout, cout_pad, k, stride=1, pad=0, dil=1, bias=None, alpha=None,
+               inv_alpha=None, residual=None, epilogue=0):
+        B, cin, tin = x.shape
+        tout = (tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
+        CALLS.append(("conv", cin, cout, k, stride, dil, tout, B,
+                      2.0 * B * cout * tout * cin * k, residual is not None))
+        return torch.empty(B, cout, tout)
+
+    def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None):
+        B, cin, tin = x.shape
+        CALLS.append(("convT", cin, cout, 2 * stride, stride, 1, tin * stride, B,
+                      2.0 * B * cin * cout * tin * 2 * stride, False))
+        return torch.empty(B, cout, tin * stride)
+
+    ops.conv1d = conv1d
+    ops.conv_transpose1d = convt
+    ops.weight_norm = lambda g, v: v
+    ops.snake_inv_alpha = lambda a: a
+    ops.pack_conv1d_weight = lambda w: (w, 128)
+    ops.pack_convt1d_weight = lambda w, s: (w, 128)
+    ops.codebook_prep = lambda cb: (cb, cb[..., 0])
+
+    def rvq_codes(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out):
+        B, D, T = z.shape
+        nq = cb.shape[0]
+        return (torch.zeros(B, nq, T, dtype=torch.long), torch.empty(B, nq * 8, T),
+                torch.empty(B, nq, T), torch.empty(B, nq, T, 8))
+
+    def rvq_expand(zst, w_out, b_out, imp=None, level=1.0, want_z_q_is=True, want_mask=True):
+        B, nq, T, d = zst.shape
+        D = w_out.shape[1]
+        return torch.empty(B, nq, D, T), torch.empty(B, D, T), torch.empty(B, nq, T)
+
+    ops.rvq_codes = rvq_codes
+    ops.rvq_expand = rvq_expand
+    ops.masked_loss = lambda l, m: torch.zeros(())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--nq", type=int, default=8)
+    args = ap.parse_args()
+    _fake()
+    import vrvq_amd
+    m = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq).eval()
+    with torch.no_grad():
+        m(torch.zeros(args.batch, 1, 44100), 44100, None, 1.0)
+    rows = list(csv.DictReader(open(args.trace)))
+    conv = [r for r in rows if "conv_mfma_kernel" in r["Kernel_Name"] or "conv_small" in r["Kernel_Name"]]
+    step = conv[-len(CALLS):]
+    tot_t = tot_f = 0.0
+    print(f"{'layer':42s} {'kernel':22s} {'us':>9s} {'GFLOP':>8s} {'TF/s':>7s} {'%pk':>5s}")
+    for c, r in zip(CALLS, step):
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        kn = r["Kernel_Name"]
+        i = kn.find("<")
+        kn = ("mfma" + kn[i:kn.find(">") + 1]) if "mfma" in kn else "small" + kn[kn.find("<"):kn.find(">") + 1]
+        tf = c[8] / (us * 1e-6) / 1e12
+        tot_t += us
+        tot_f += c[8]
+        desc = f"{c[0]} {c[1]}->{c[2]} k{c[3]} s{c[4]} d{c[5]} T{c[6]}{' +res' if c[9] else ''}"
+        print(f"{desc:42s} {kn:22s} {us:9.1f} {c[8]/1e9:8.1f} {tf:7.1f} {tf/157.3*100:5.1f}")
+    print(f"total conv: {tot_t/1e3:.2f} ms, {tot_f/1e12:.3f} TFLOP, {tot_f/(tot_t*1e-6)/1e12:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
