@@ -80,11 +80,19 @@ int vrvq_codebook_prep(const float* cb, int rows, int dim, float* cbn, float* c2
  * w_packed: [Cin][k][cout_pad] (cout_pad >= Cout, multiple of 128, zero padded) as produced
  * by vrvq_pack_conv1d_weight. residual (nullable) has the output's shape.
  * tout must equal floor((tin + 2*pad - dil*(k-1) - 1)/stride) + 1.
+ *
+ * Producer-side Snake: when y_snake != NULL the epilogue also writes
+ *   y_snake[b,co,t] = snake_co(y[b,co,t]) with alpha_out / inv_alpha_out ([Cout]),
+ * i.e. the Snake1d that the NEXT layer applies to this output (models/layers.py:52-110: every
+ * consumer of a conv output starts with a Snake). The consumer then runs with alpha == NULL,
+ * so the activation is evaluated once per element instead of once per consumer tile. y may be
+ * NULL when only the activated tensor is needed (it must not be NULL otherwise).
  * ------------------------------------------------------------------------------------- */
 int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 const float* inv_alpha, const float* w_packed, int cout, int cout_pad, int k,
                 int stride, int pad, int dil, const float* bias, const float* residual,
-                int epilogue, float* y, int tout, vrvq_stream_t stream);
+                int epilogue, float* y, int tout, const float* alpha_out,
+                const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
 /* Pack a folded Conv1d weight w[Cout][Cin][k] into [Cin][k][cout_pad]. */
 int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
@@ -94,10 +102,12 @@ int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_p
  * the DecoderBlock upsampler (models/layers.py:92-103): y has length tin*stride.
  * Computed as a polyphase 2-tap conv with cout*stride phase-channels:
  *   y[b,co,m*s+r-p] = bias[co] + sum_ci W[ci,co,r]*xs[ci,m] + W[ci,co,r+s]*xs[ci,m-1].
- * w_packed from vrvq_pack_convt1d_weight ([Cin][2][cout*stride padded to 128]). */
+ * w_packed from vrvq_pack_convt1d_weight ([Cin][2][cout*stride padded to 128]).
+ * alpha_out / inv_alpha_out / y_snake: producer-side Snake as in vrvq_conv1d. */
 int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin, const float* alpha,
                           const float* inv_alpha, const float* w_packed, int cout,
                           int cout_pad, int stride, const float* bias, float* y,
+                          const float* alpha_out, const float* inv_alpha_out, float* y_snake,
                           vrvq_stream_t stream);
 
 /* Pack a folded ConvTranspose1d weight w[Cin][Cout][2*stride] into the polyphase layout. */

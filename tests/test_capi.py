@@ -57,11 +57,14 @@ def test_argument_errors_raise_before_launch():
     # null pointers -> VRVQ_ERR_ARG, returned by the host-side check (no GPU touched)
     assert lib.vrvq_weight_norm(None, None, 4, 4, None, None) == 10001
     assert lib.vrvq_conv1d(None, 1, 1, 8, None, None, None, 1, 128, 3, 1, 1, 1, None, None, 0,
-                           None, 8, None) == 10001
+                           None, 8, None, None, None, None) == 10001
     assert lib.vrvq_rvq_codes(*([None] + [1] * 6 + [None] * 12)) == 10001
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
     # geometry mismatch (tout inconsistent with the conv formula)
     p = ctypes.c_void_p(16)
     assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, 4, 128, 7, 1, 3, 1, None, None, 0,
-                           p, 99, None) == 10001
+                           p, 99, None, None, None, None) == 10001
+    # producer-side snake without its alpha
+    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, 4, 128, 7, 1, 3, 1, None, None, 0,
+                           None, 100, None, None, p, None) == 10001

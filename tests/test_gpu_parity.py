@@ -177,6 +177,19 @@ def test_conv1d_vs_torch(case):
                    residual=res, epilogue=epi)
     assert y.shape == ref.shape
     assert rel_err(y.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    # producer-side Snake of the next layer: bit-identical to snake applied to the stored y
+    a_next = (torch.rand(cout, generator=gen) * 1.5 + 0.5).to(DEV)
+    for want_raw in (True, False):
+        y2, ys = ops.conv1d(x, wp, cout, cout_pad, k, s, p, d, bias=b,
+                            alpha=alpha if use_snake else None,
+                            inv_alpha=ops.snake_inv_alpha(alpha) if use_snake else None,
+                            residual=res, epilogue=epi,
+                            out_snake=(a_next, ops.snake_inv_alpha(a_next)), want_raw=want_raw)
+        if want_raw:
+            assert torch.equal(y2, y)
+        else:
+            assert y2 is None
+        assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
 
 
 @pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8), (2, 384, 192, 333, 4),
@@ -195,6 +208,12 @@ def test_conv_transpose1d_vs_torch(case):
                              inv_alpha=ops.snake_inv_alpha(alpha))
     assert y.shape == ref.shape
     assert rel_err(y.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    a_next = (torch.rand(cout, generator=gen) * 1.5 + 0.5).to(DEV)
+    y2, ys = ops.conv_transpose1d(x, wp, cout, cout_pad, s, bias=b, alpha=alpha,
+                                  inv_alpha=ops.snake_inv_alpha(alpha),
+                                  out_snake=(a_next, ops.snake_inv_alpha(a_next)))
+    assert torch.equal(y2, y)
+    assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
 
 
 def test_weight_norm_and_codebook_prep_vs_torch():

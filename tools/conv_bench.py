@@ -25,17 +25,23 @@ def main():
     ap.add_argument("--res", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--convt", type=int, default=0, help="transposed conv with this stride")
+    ap.add_argument("--snake-in", action="store_true", help="Snake on load (consumer side)")
+    ap.add_argument("--no-snake-out", action="store_true", help="no producer-side Snake output")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
     x = (torch.rand(args.batch, args.cin, args.t, generator=g) - 0.5).to(dev)
     alpha = (torch.rand(args.cin, generator=g) + 0.5).to(dev)
     inv = ops.snake_inv_alpha(alpha)
+    a_in, i_in = (alpha, inv) if args.snake_in else (None, None)
+    ao = (torch.rand(args.cout, generator=g) + 0.5).to(dev)
+    osn = None if args.no_snake_out else (ao, ops.snake_inv_alpha(ao))
     if args.convt:
         w = (torch.randn(args.cin, args.cout, 2 * args.convt, generator=g) * 0.02).to(dev)
         wp, cp = ops.pack_convt1d_weight(w, args.convt)
         b = torch.zeros(args.cout, device=dev)
-        fn = lambda: ops.conv_transpose1d(x, wp, args.cout, cp, args.convt, b, alpha, inv)
+        fn = lambda: ops.conv_transpose1d(x, wp, args.cout, cp, args.convt, b, a_in, i_in,
+                                          out_snake=osn, want_raw=True)
         flops = 2.0 * args.batch * args.cin * args.cout * 2 * args.convt * args.t
     else:
         w = (torch.randn(args.cout, args.cin, args.k, generator=g) * 0.02).to(dev)
@@ -44,8 +50,8 @@ def main():
         pad = (args.k - 1) * args.dil // 2 if args.stride == 1 else (args.stride + 1) // 2
         tout = (args.t + 2 * pad - args.dil * (args.k - 1) - 1) // args.stride + 1
         res = torch.randn(args.batch, args.cout, tout, device=dev) if args.res else None
-        fn = lambda: ops.conv1d(x, wp, args.cout, cp, args.k, args.stride, pad, args.dil, b, alpha,
-                                inv, res)
+        fn = lambda: ops.conv1d(x, wp, args.cout, cp, args.k, args.stride, pad, args.dil, b, a_in,
+                                i_in, res, out_snake=osn, want_raw=args.res or osn is None)
         flops = 2.0 * args.batch * args.cin * args.cout * args.k * tout
     for _ in range(3):
         fn()

@@ -22,18 +22,21 @@ CALLS = []
 
 def _fake():
     def conv1d(x, wp, cout, cout_pad, k, stride=1, pad=0, dil=1, bias=None, alpha=None,
-               inv_alpha=None, residual=None, epilogue=0):
+               inv_alpha=None, residual=None, epilogue=0, out_snake=None, want_raw=True):
         B, cin, tin = x.shape
         tout = (tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
         CALLS.append(("conv", cin, cout, k, stride, dil, tout, B,
                       2.0 * B * cout * tout * cin * k, residual is not None))
-        return torch.empty(B, cout, tout)
+        y = torch.empty(B, cout, tout)
+        return y if out_snake is None else (y, torch.empty_like(y))
 
-    def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None):
+    def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None,
+              out_snake=None, want_raw=True):
         B, cin, tin = x.shape
         CALLS.append(("convT", cin, cout, 2 * stride, stride, 1, tin * stride, B,
                       2.0 * B * cin * cout * tin * 2 * stride, False))
-        return torch.empty(B, cout, tin * stride)
+        y = torch.empty(B, cout, tin * stride)
+        return y if out_snake is None else (y, torch.empty_like(y))
 
     ops.conv1d = conv1d
     ops.conv_transpose1d = convt

@@ -22,9 +22,10 @@ SIGNATURES = {
     "vrvq_weight_norm": [_P, _P, _I, _I, _P, _P],
     "vrvq_snake_inv_alpha": [_P, _I, _P, _P],
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
-    "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I, _P],
+    "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
+                    _P, _P, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
-    "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
     "vrvq_rvq_codes": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "vrvq_rvq_expand": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],

@@ -15,6 +15,7 @@
 // :52-110 (ResidualUnit skip, EncoderBlock, DecoderBlock), models/dac_vrvq.py:19-80,
 // models/importance_subnet.py:38-45.
 #include "common.h"
+#include <stdlib.h>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -27,7 +28,10 @@ struct ConvArgs {
   const float* w;          // [cin][KS][m_pad]
   const float* bias;       // [cout] or null
   const float* res;        // [B][cout][ylen] or null
-  float* y;                // [B][cout][ylen]
+  float* y;                // [B][cout][ylen] or null
+  const float* alpha_o;    // [cout] snake of the NEXT layer, applied in the epilogue, or null
+  const float* inv_alpha_o;
+  float* ys;               // [B][cout][ylen] snake_o(y), or null
   int cin, tin;
   int M;                   // GEMM rows: cout (normal) or cout*up (transposed)
   int m_pad;
@@ -65,9 +69,20 @@ struct WinCfg {
   static constexpr int PER_ROW = (XW_MAX + 63) / 64;  // positions per lane per row
 };
 
-template <int BM, int BN, int WM, int KS>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
-  constexpr int WN = 4 / WM;
+// Epilogue column passes: the accumulator tile goes through LDS in BM x (BN / EPASS) pieces of
+// at most 64 KiB, EPASS dividing the wave-column count.
+template <int BM, int BN, int WN>
+struct EpiCfg {
+  static constexpr int need = (BM * BN * 4 + 65535) / 65536;
+  static constexpr int EPASS = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+  static_assert(WN % EPASS == 0 || EPASS == 1, "epilogue passes must split the wave columns");
+  static constexpr int BNP = BN / EPASS;
+};
+
+template <int BM, int BN, int WM, int NW, int KS>
+__global__ __launch_bounds__(64 * NW) void conv_mfma_kernel(ConvArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = NW / WM;
   constexpr int TM = BM / WM;
   constexpr int TN = BN / WN;
   constexpr int RM = TM / 32;
@@ -75,15 +90,18 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   constexpr int CK = ChunkCfg<KS, BM>::CK;
   constexpr int KROWS = CK * KS;
   constexpr int WQ4 = KROWS * BM / 4;               // float4 of W per chunk
-  constexpr int WQ = (WQ4 + 255) / 256;             // ... per thread
-  constexpr int XROWS = CK / 4;                     // x rows per wave per chunk
+  constexpr int WQ = (WQ4 + NT - 1) / NT;           // ... per thread
+  constexpr int XROWS = (CK + NW - 1) / NW;         // x rows per wave per chunk
   constexpr int XPR = WinCfg<KS, BN>::PER_ROW;
+  constexpr int EPASS = EpiCfg<BM, BN, WN>::EPASS;
+  constexpr int BNP = EpiCfg<BM, BN, WN>::BNP;
+  static_assert(NW * 64 == NT && WM * WN == NW, "waves");
   static_assert(RM >= 1 && RN >= 1 && TM % 32 == 0 && TN % 32 == 0, "tile");
-  static_assert(CK % 4 == 0, "chunk shape");
+  static_assert(CK % 2 == 0, "chunk shape");
 
   // Two LDS stages: [W chunk | x window] x 2. The next chunk is prefetched into registers
-  // while the current one feeds the MFMAs, then written (with Snake) to the other stage:
-  // one barrier per K-chunk.
+  // while the current one feeds the MFMAs, then written to the other stage: one barrier per
+  // K-chunk.
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
   // Strided convs store the window phase-split, [phase][position / stride], so the B-operand
@@ -118,6 +136,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 
   const float* xb = a.x + (size_t)b * a.cin * a.tin;
   const int xbase = n0 * a.stride - a.pad;
+  // Wave-uniform fast paths: every chunk holds CK real channels, and the window lies inside
+  // [0, tin) (no zero padding): the loads then need no per-lane predicates.
+  const bool cin_full = a.cin % CK == 0;
+  const bool interior = cin_full && xbase >= 0 && xbase + XW <= a.tin;
 
   float4 wreg[WQ];
   float xreg[XROWS][XPR];
@@ -125,22 +147,36 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   auto load_chunk = [&](int ci0) {
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
-      const int idx = tid + q * 256;
+      const int idx = tid + q * NT;
       const int rr = idx / (BM / 4);
       const int cc = (idx - rr * (BM / 4)) * 4;
-      wreg[q] = (idx < WQ4 && ci0 + rr / KS < a.cin)
-                    ? *reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4* src = reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc);
+      if (WQ4 % NT == 0 && cin_full) wreg[q] = *src;
+      else wreg[q] = (idx < WQ4 && ci0 + rr / KS < a.cin) ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if (interior) {
 #pragma unroll
-    for (int rw = 0; rw < XROWS; ++rw) {
-      const int ci = ci0 + wave + 4 * rw;
-      const float* xr = xb + (size_t)ci * a.tin;
+      for (int rw = 0; rw < XROWS; ++rw) {
+        const int cl = wave + NW * rw;
+        const float* xr = xb + (size_t)(ci0 + cl) * a.tin + xbase;
 #pragma unroll
-      for (int u = 0; u < XPR; ++u) {
-        const int p = lane + 64 * u;
-        const int t = xbase + p;
-        xreg[rw][u] = (ci < a.cin && p < XW && t >= 0 && t < a.tin) ? xr[t] : 0.0f;
+        for (int u = 0; u < XPR; ++u) {
+          const int p = lane + 64 * u;
+          xreg[rw][u] = (cl < CK && p < XW) ? xr[p] : 0.0f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int rw = 0; rw < XROWS; ++rw) {
+        const int cl = wave + NW * rw;
+        const int ci = ci0 + cl;
+        const float* xr = xb + (size_t)ci * a.tin;
+#pragma unroll
+        for (int u = 0; u < XPR; ++u) {
+          const int p = lane + 64 * u;
+          const int t = xbase + p;
+          xreg[rw][u] = (cl < CK && ci < a.cin && p < XW && t >= 0 && t < a.tin) ? xr[t] : 0.0f;
+        }
       }
     }
   };
@@ -149,10 +185,11 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     float* xs = stg + KROWS * BM;
 #pragma unroll
     for (int q = 0; q < WQ; ++q)
-      if (tid + q * 256 < WQ4) reinterpret_cast<float4*>(ws)[tid + q * 256] = wreg[q];
+      if (WQ4 % NT == 0 || tid + q * NT < WQ4) reinterpret_cast<float4*>(ws)[tid + q * NT] = wreg[q];
 #pragma unroll
     for (int rw = 0; rw < XROWS; ++rw) {
-      const int cl = wave + 4 * rw;
+      const int cl = wave + NW * rw;
+      if (cl >= CK) continue;
       const int ci = ci0 + cl;
       const bool sn = a.alpha != nullptr && ci < a.cin;
       const float al = sn ? a.alpha[ci] : 0.f, ia = sn ? a.inv_alpha[ci] : 0.f;
@@ -180,24 +217,43 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     const float* ws = smem + cur * STG;
     const float* xs = ws + KROWS * BM;
     // ---- MFMA over the chunk: K order = (tap, channel pair) ----
+    // Software-pipelined: the LDS operands of step s+1 are read before the MFMAs of step s
+    // are issued, so the ds_read latency hides behind the MFMAs instead of stalling every
+    // step on lgkmcnt(0).
+    constexpr int CP = CK / 2;
+    constexpr int NSTEP = KS * CP;
+    const int col = wn * TN + lr;
+    auto rd = [&](int st, float (&av)[RM], float (&bv)[RN]) {
+      const int k = st / CP, kr = (st % CP) * 2 + lh;
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
+      for (int i = 0; i < RM; ++i) av[i] = ws[(kr * KS + k) * BM + wm * TM + i * 32 + lr];
+      const int xo = a.ssh ? kr * XWP + (k & (a.stride - 1)) * XP + col + (k >> a.ssh)
+                           : kr * XWP + col + k * a.dil;
 #pragma unroll
-      for (int cc = 0; cc < CK; cc += 2) {
-        const int kr = cc + lh;
-        float av[RM], bv[RN];
+      for (int j = 0; j < RN; ++j) bv[j] = xs[xo + j * 32];
+    };
+    auto mma = [&](const float (&av)[RM], const float (&bv)[RN]) {
 #pragma unroll
-        for (int i = 0; i < RM; ++i) av[i] = ws[(kr * KS + k) * BM + wm * TM + i * 32 + lr];
-        const int col = wn * TN + lr;
-        const int xo = a.ssh ? kr * XWP + (k & (a.stride - 1)) * XP + col + (k >> a.ssh)
-                             : kr * XWP + col + k * a.dil;
+      for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bv[j] = xs[xo + j * 32];
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    {
+      float a0[RM], b0[RN], a1[RM], b1[RN];
+      rd(0, a0, b0);
 #pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      for (int st = 0; st < NSTEP; st += 2) {
+        // sched_barrier(0): keep each read group ahead of the MFMAs it overlaps (the
+        // scheduler otherwise sinks the reads to the MFMAs that consume them).
+        if (st + 1 < NSTEP) rd(st + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < NSTEP) rd(st + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < NSTEP) mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (more) store_chunk(smem + (cur ^ 1) * STG, ci0 + CK);
@@ -205,66 +261,114 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     cur ^= 1;
   }
 
-  // ---- epilogue: bias, residual, activation, store ----
-  // Per accumulator tile: every load (bias, residual) is issued before any store, so the
-  // 16 round trips overlap instead of serialising behind possibly-aliasing stores.
-  if (a.up == 0) {
+  // ---- epilogue through LDS (every stage buffer is free after the loop's last barrier) ----
+  // The accumulator tile is transposed to row-major [BM][BNP] (EPASS column passes) so that
+  // each wave then handles 64 consecutive output positions of one row: residual loads and
+  // y / snake(y) stores are 256-B coalesced, and the per-element Snake of the next layer runs
+  // in a rolled loop.
+  float* ct = smem;
+  const int mrows = min(BM, a.M - m0);
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int mb = m0 + wm * TM + i * 32 + 4 * lh;
-      float bv[16];
+  for (int pass = 0; pass < EPASS; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wn / (WN / EPASS) == pass) {
+      const int cbase = wn * TN - pass * BNP;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2);
-        bv[r] = (a.bias && m < a.M) ? a.bias[m] : 0.0f;
-      }
+      for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int n = n0 + wn * TN + j * 32 + lr;
-        const size_t ob = ((size_t)b * a.cout + mb) * a.ylen + n;
-        float v[16];
+        for (int j = 0; j < RN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = acc[i][j][r] + bv[r];
-        if (a.res) {
-          float rv[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int mo = (r & 3) + 8 * (r >> 2);
-            rv[r] = (mb + mo < a.M && n < a.ng) ? a.res[ob + (size_t)mo * a.ylen] : 0.0f;
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = rv[r] + v[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mo = (r & 3) + 8 * (r >> 2);
-          if (mb + mo < a.M && n < a.ng) a.y[ob + (size_t)mo * a.ylen] = apply_epi(v[r], a.epi);
-        }
-      }
+          for (int r = 0; r < 16; ++r)
+            ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * BNP + cbase + j * 32 + lr] =
+                acc[i][j][r];
     }
-  } else {
-    // transposed conv: GEMM row m = co*up + phase, output t = n*up + phase - up_pad
+    __syncthreads();
+    const int p0 = n0 + pass * BNP;  // first GEMM column of this pass
+    if (a.up == 0) {
+      // Each thread owns 4 consecutive columns per step; U steps are loaded (accumulator
+      // tile, bias, residual, next-layer alpha) before anything is stored, so the global
+      // loads of a step group are in flight together.
+      constexpr int NV = BNP / 4;
+      constexpr int ITER = (BM * NV + NT - 1) / NT;
+      constexpr int U = ITER >= 4 ? 4 : ITER;
+      const int ncols = min(BNP, a.ng - p0);
+      const bool vec = (a.ylen & 3) == 0;
+      for (int it0 = 0; it0 < ITER; it0 += U) {
+        float v[U][4], sa[U], si[U];
+        size_t ob[U];
+        int nl[U];
+        bool ok[U], full[U];
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int mb = m0 + wm * TM + i * 32 + 4 * lh;
-      int cor[16], phr[16];
-      float bv[16];
+        for (int u = 0; u < U; ++u) {
+          const int e = tid + NT * (it0 + u);
+          const int ml = e / NV;
+          nl[u] = (e - ml * NV) * 4;
+          ok[u] = it0 + u < ITER && ml < mrows && nl[u] < ncols;
+          full[u] = vec && nl[u] + 4 <= ncols;
+          const int m = ok[u] ? m0 + ml : m0;
+          const float4 c = ok[u] ? *reinterpret_cast<const float4*>(ct + ml * BNP + nl[u])
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float bb = (a.bias && ok[u]) ? a.bias[m] : 0.0f;
+          v[u][0] = c.x + bb; v[u][1] = c.y + bb; v[u][2] = c.z + bb; v[u][3] = c.w + bb;
+          ob[u] = ((size_t)b * a.cout + m) * a.ylen + p0 + nl[u];
+          sa[u] = (a.ys && ok[u]) ? a.alpha_o[m] : 0.0f;
+          si[u] = (a.ys && ok[u]) ? a.inv_alpha_o[m] : 0.0f;
+          if (a.res && ok[u]) {
+            if (full[u]) {
+              const float4 r = *reinterpret_cast<const float4*>(a.res + ob[u]);
+              v[u][0] = r.x + v[u][0]; v[u][1] = r.y + v[u][1];
+              v[u][2] = r.z + v[u][2]; v[u][3] = r.w + v[u][3];
+            } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2);
-        const int co = m / a.up;
-        cor[r] = m < a.M ? co : -1;
-        phr[r] = m - co * a.up - a.up_pad;
-        bv[r] = (a.bias && m < a.M) ? a.bias[co] : 0.0f;
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) v[u][q] = a.res[ob[u] + q] + v[u][q];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] = apply_epi(v[u][q], a.epi);
+          if (a.y && ok[u]) {
+            if (full[u]) {
+              *reinterpret_cast<float4*>(a.y + ob[u]) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) a.y[ob[u] + q] = v[u][q];
+            }
+          }
+        }
+        if (a.ys) {
+          for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            float sv[4];
+            for (int q = 0; q < 4; ++q) sv[q] = snake_act(v[u][q], sa[u], si[u]);
+            if (full[u]) {
+              *reinterpret_cast<float4*>(a.ys + ob[u]) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+            } else {
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) a.ys[ob[u] + q] = sv[q];
+            }
+          }
+        }
       }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int n = n0 + wn * TN + j * 32 + lr;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int t = n * a.up + phr[r];
-          if (cor[r] >= 0 && n < a.ng && t >= 0 && t < a.ylen)
-            a.y[((size_t)b * a.cout + cor[r]) * a.ylen + t] = acc[i][j][r] + bv[r];
+    } else {
+      // transposed conv: GEMM row m = co*up + phase, column n -> t = n*up + phase - up_pad.
+      // Walk (channel, t) so consecutive lanes store consecutive t.
+      const int up = a.up, tl_n = BNP * up;
+      const int co0 = m0 / up, nco = min(BM / up, a.cout - co0);
+      for (int e = tid; e < BM * BNP; e += NT) {
+        const int cl = e / tl_n, tl = e - cl * tl_n;
+        const int nl = tl / up, ph = tl - nl * up;
+        const int t = (p0 + nl) * up + ph - a.up_pad;
+        if (cl < nco && p0 + nl < a.ng && t >= 0 && t < a.ylen) {
+          const int co = co0 + cl;
+          float v = ct[(cl * up + ph) * BNP + nl];
+          if (a.bias) v = v + a.bias[co];
+          const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
+          if (a.y) a.y[o] = v;
+          if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[co], a.inv_alpha_o[co]);
         }
       }
     }
@@ -333,7 +437,9 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
         if (a.bias) v = v + a.bias[c];
         const size_t o = ((size_t)b * a.cout + c) * a.ylen + t;
         if (a.res) v = a.res[o] + v;
-        a.y[o] = apply_epi(v, a.epi);
+        v = apply_epi(v, a.epi);
+        if (a.y) a.y[o] = v;
+        if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[c], a.inv_alpha_o[c]);
       }
     }
   }
@@ -352,7 +458,7 @@ int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
   return vrvq_launch_status();
 }
 
-template <int BM, int BN, int WM, int KS>
+template <int BM, int BN, int WM, int NW, int KS>
 int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   ConvArgs a = a0;
   a.n_mt = (a.M + BM - 1) / BM;
@@ -363,18 +469,28 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
   const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
   if (XW > 64 * WinCfg<KS, BN>::PER_ROW) return VRVQ_ERR_UNSUPPORTED;  // window > staged lanes
-  const size_t lds = 2 * (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
+  size_t lds = 2 * (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
+  const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
+  if (lds < epi) lds = epi;  // epilogue tile
   if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, KS>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
   const long long nblk = (long long)a.n_mt * a.n_nt * batch;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, KS>), dim3((unsigned)nblk), dim3(256), lds,
-                     st, a);
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS>), dim3((unsigned)nblk), dim3(64 * NW),
+                     lds, st, a);
   return vrvq_launch_status();
+}
+
+static int conv_variant() {  // tuning override: VRVQ_CONV_VARIANT=0 (4-wave) | 1 (8-wave wide)
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
@@ -391,18 +507,28 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   }
   else if (a.ng < 4096 && waste(64) * 10 < waste(128) * 7) bn = 64;
   else bn = 128;
-  if (a.M <= 32) return launch_cfg<32, 128, 1, KS>(a, batch, st);
-  if (bn == 32) return launch_cfg<128, 32, 4, KS>(a, batch, st);
-  if (bn == 96) return launch_cfg<128, 96, 4, KS>(a, batch, st);
+  if (a.M <= 32) return launch_cfg<32, 128, 1, 4, KS>(a, batch, st);
+  if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
+  if (bn == 96) return launch_cfg<128, 96, 4, 4, KS>(a, batch, st);
+  constexpr bool kWide = KS == 1 || KS == 2 || KS == 3 || KS == 7;  // register budget at 512 threads
+  const bool wide = kWide && conv_variant() == 1 && bn == 128 && a.ng >= 4096;
   if (a.M <= 64) {
-    if (bn == 64) return launch_cfg<64, 64, 2, KS>(a, batch, st);
-    return launch_cfg<64, 128, 2, KS>(a, batch, st);
+    if (bn == 64) return launch_cfg<64, 64, 2, 4, KS>(a, batch, st);
+    if constexpr (kWide) if (wide) return launch_cfg<64, 256, 2, 8, KS>(a, batch, st);
+    return launch_cfg<64, 128, 2, 4, KS>(a, batch, st);
   }
   // 96- and 192-row tiles: no padded rows for the C = 96 / 192 decoder blocks
-  if (a.M <= 96) return launch_cfg<96, 128, 1, KS>(a, batch, st);
-  if (KS >= 3 && a.M % 128 != 0 && a.M % 192 == 0) return launch_cfg<192, 128, 2, KS>(a, batch, st);
-  if (bn == 64) return launch_cfg<128, 64, 2, KS>(a, batch, st);
-  return launch_cfg<128, 128, 2, KS>(a, batch, st);
+  if (a.M <= 96) {
+    if constexpr (kWide) if (wide) return launch_cfg<96, 256, 1, 8, KS>(a, batch, st);
+    return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
+  }
+  if (KS >= 3 && a.M % 128 != 0 && a.M % 192 == 0) {
+    if constexpr (kWide) if (wide) return launch_cfg<192, 256, 2, 8, KS>(a, batch, st);
+    return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+  }
+  if (bn == 64) return launch_cfg<128, 64, 2, 4, KS>(a, batch, st);
+  if constexpr (kWide) if (wide) return launch_cfg<128, 256, 2, 8, KS>(a, batch, st);
+  return launch_cfg<128, 128, 2, 4, KS>(a, batch, st);
 }
 
 int dispatch_ks(int ks, const ConvArgs& a, int batch, hipStream_t st) {
@@ -458,8 +584,10 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
                            const float* inv_alpha, const float* w_packed, int cout,
                            int cout_pad, int k, int stride, int pad, int dil, const float* bias,
                            const float* residual, int epilogue, float* y, int tout,
+                           const float* alpha_out, const float* inv_alpha_out, float* y_snake,
                            vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(x && w_packed && y);
+  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
+  VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && stride > 0 &&
                  dil > 0 && pad >= 0 && tout > 0);
   VRVQ_CHECK_ARG(cout_pad >= cout && cout_pad % 128 == 0);
@@ -470,6 +598,7 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   ConvArgs a{};
   a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
   a.res = residual; a.y = y;
+  a.alpha_o = alpha_out; a.inv_alpha_o = inv_alpha_out; a.ys = y_snake;
   a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
   a.stride = stride; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0;
   a.ssh = 0;
@@ -484,8 +613,11 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
 extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin,
                                      const float* alpha, const float* inv_alpha,
                                      const float* w_packed, int cout, int cout_pad, int stride,
-                                     const float* bias, float* y, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(x && w_packed && y);
+                                     const float* bias, float* y, const float* alpha_out,
+                                     const float* inv_alpha_out, float* y_snake,
+                                     vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
+  VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && stride > 0);
   VRVQ_CHECK_ARG(cout_pad >= cout * stride && cout_pad % 128 == 0);
   VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
@@ -493,6 +625,7 @@ extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin
   ConvArgs a{};
   a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
   a.res = nullptr; a.y = y;
+  a.alpha_o = alpha_out; a.inv_alpha_o = inv_alpha_out; a.ys = y_snake;
   a.cin = cin; a.tin = tin; a.M = cout * stride; a.m_pad = cout_pad; a.cout = cout;
   a.stride = 1; a.pad = 1; a.dil = 1; a.ng = tin + 1; a.up = stride; a.up_pad = p;
   a.ylen = (tin - 1) * stride - 2 * p + 2 * stride;

@@ -88,7 +88,10 @@ class WNConv1d(nn.Module):
         return self._cache[1], self._cache[2]
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
-                residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE):
+                residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE,
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
+        """conv(snake(x)) (+ residual, epilogue). With out_snake (the consumer's Snake1d)
+        returns (y or None, out_snake(y)) computed in the same epilogue."""
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
@@ -96,7 +99,9 @@ class WNConv1d(nn.Module):
         return ops.conv1d(x, wp, self.out_channels, cout_pad, self.kernel_size[0],
                           self.stride[0], self.padding[0], self.dilation[0],
                           bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
-                          residual=residual, epilogue=epilogue)
+                          residual=residual, epilogue=epilogue,
+                          out_snake=None if out_snake is None else out_snake.prepared(),
+                          want_raw=want_raw)
 
 
 class WNConvTranspose1d(nn.Module):
@@ -130,13 +135,16 @@ class WNConvTranspose1d(nn.Module):
             self._cache = (key, wp, cout_pad)
         return self._cache[1], self._cache[2]
 
-    def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None):
+    def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
             alpha, inv = snake.prepared()
         return ops.conv_transpose1d(x, wp, self.out_channels, cout_pad, self.stride[0],
-                                    bias=self.bias.detach(), alpha=alpha, inv_alpha=inv)
+                                    bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
+                                    out_snake=None if out_snake is None else out_snake.prepared(),
+                                    want_raw=want_raw)
 
 
 class ResidualUnit(nn.Module):
@@ -156,6 +164,13 @@ class ResidualUnit(nn.Module):
         y = self.block[1](x, snake=self.block[0])
         # "same" padding: the reference's centre crop (:65-67) never triggers.
         return self.block[3](y, snake=self.block[2], residual=x)
+
+    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool):
+        """Chained form: x_snk = block[0](x) was produced by the previous layer's epilogue.
+        The k7 conv writes only block[2](h) (h has no other consumer); the k1 conv adds the
+        skip and writes (y if want_raw, out_snake(y)) for the next layer."""
+        _, h_snk = self.block[1](x_snk, out_snake=self.block[2], want_raw=False)
+        return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw)
 
 
 class EncoderBlock(nn.Module):
@@ -177,6 +192,17 @@ class EncoderBlock(nn.Module):
             x = self.block[i](x)
         return self.block[4](x, snake=self.block[3])
 
+    def entry_snake(self) -> Snake1d:
+        return self.block[0].block[0]
+
+    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Optional[Snake1d],
+            want_raw: bool):
+        """Chained form (see ResidualUnit.run); returns what block[4] returns."""
+        for i in range(3):
+            nxt = self.block[i + 1].block[0] if i < 2 else self.block[3]
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=i < 2)
+        return self.block[4](x_snk, out_snake=out_snake, want_raw=want_raw)
+
 
 class DecoderBlock(nn.Module):
     """Snake, ConvTranspose k=2s (x s upsampling), 3 residual units (models/layers.py:92-110)."""
@@ -197,3 +223,16 @@ class DecoderBlock(nn.Module):
         for i in range(2, 5):
             x = self.block[i](x)
         return x
+
+    def entry_snake(self) -> Snake1d:
+        return self.block[0]
+
+    def run(self, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool = False):
+        """Chained form: x_snk = block[0](x) from the previous epilogue; returns
+        (y or None, out_snake(y))."""
+        x, x_snk = self.block[1](x_snk, out_snake=self.block[2].block[0], want_raw=True)
+        for i in range(2, 5):
+            last = i == 4
+            nxt = out_snake if last else self.block[i + 1].block[0]
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=want_raw if last else True)
+        return x, x_snk

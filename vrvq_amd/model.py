@@ -33,10 +33,15 @@ class Encoder(nn.Module):
         self.block = nn.Sequential(*blocks)
 
     def forward(self, x, return_feat: bool = False):
+        # Chained launches: every conv's epilogue also writes the next Snake's output, so each
+        # activation is evaluated once per element (include/vrvq.h, producer-side Snake).
         n = len(self.block)
-        x = self.block[0](x)
+        x, x_snk = self.block[0](x, out_snake=self.block[1].entry_snake())
         for i in range(1, n - 2):
-            x = self.block[i](x)
+            last = i == n - 3
+            nxt = None if last else self.block[i + 1].entry_snake()
+            r = self.block[i].run(x, x_snk, nxt, want_raw=True)
+            x, x_snk = (r, None) if last else r
         feat = x  # output of block index n-3 (the last EncoderBlock), models/dac_vrvq.py:43-44
         out = self.block[n - 1](x, snake=self.block[n - 2])
         return (out, feat) if return_feat else out
@@ -59,10 +64,11 @@ class Decoder(nn.Module):
 
     def forward(self, x):
         n = len(self.model)
-        x = self.model[0](x)
+        _, x_snk = self.model[0](x, out_snake=self.model[1].entry_snake(), want_raw=False)
         for i in range(1, n - 3):
-            x = self.model[i](x)
-        return self.model[n - 2](x, snake=self.model[n - 3], epilogue=ops.EPI_TANH)
+            nxt = self.model[n - 3] if i == n - 4 else self.model[i + 1].entry_snake()
+            _, x_snk = self.model[i].run(x_snk, nxt, want_raw=False)
+        return self.model[n - 2](x_snk, epilogue=ops.EPI_TANH)
 
 
 # ============================================================================ importance subnet

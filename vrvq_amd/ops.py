@@ -98,8 +98,13 @@ def pack_convt1d_weight(w: torch.Tensor, stride: int) -> Tuple[torch.Tensor, int
 def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k: int,
            stride: int = 1, pad: int = 0, dil: int = 1, bias: Optional[torch.Tensor] = None,
            alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
-           residual: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE) -> torch.Tensor:
-    """y = epi(residual + conv1d(snake(x)) + bias) on the MFMA implicit-GEMM kernel."""
+           residual: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
+           out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, want_raw: bool = True):
+    """y = epi(residual + conv1d(snake(x)) + bias) on the MFMA implicit-GEMM kernel.
+
+    out_snake = (alpha_next, inv_alpha_next) also produces snake_next(y) from the epilogue
+    (the next layer's Snake). Returns y, or (y | None, snake_next(y)) when out_snake is given
+    (y is None when want_raw is False)."""
     _chk(x, "x"); dev = x.device
     for t, n in ((w_packed, "w_packed"), (bias, "bias"), (alpha, "alpha"),
                  (inv_alpha, "inv_alpha"), (residual, "residual")):
@@ -114,27 +119,45 @@ def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k:
         raise RuntimeError("conv1d: residual shape must equal the output shape")
     if alpha is not None and inv_alpha is None:
         raise RuntimeError("conv1d: snake needs inv_alpha")
-    y = torch.empty((B, cout, tout), device=dev, dtype=torch.float32)
+    ao, io, ys = _out_snake(out_snake, (B, cout, tout), dev)
+    y = torch.empty((B, cout, tout), device=dev, dtype=torch.float32) \
+        if (want_raw or out_snake is None) else None
     _lib.call("vrvq_conv1d", _p(x), B, cin, tin, _p(alpha), _p(inv_alpha), _p(w_packed), cout,
               cout_pad, k, stride, pad, dil, _p(bias), _p(residual), int(epilogue), _p(y), tout,
-              _stream(x))
-    return y
+              _p(ao), _p(io), _p(ys), _stream(x))
+    return y if out_snake is None else (y, ys)
+
+
+def _out_snake(out_snake, shape, dev):
+    if out_snake is None:
+        return None, None, None
+    ao, io = out_snake
+    _chk(ao, "alpha_out", device=dev); _chk(io, "inv_alpha_out", device=dev)
+    if ao.numel() != shape[1] or io.numel() != shape[1]:
+        raise RuntimeError("out_snake: one alpha per output channel")
+    return ao, io, torch.empty(shape, device=dev, dtype=torch.float32)
 
 
 def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int,
                      stride: int, bias: Optional[torch.Tensor] = None,
                      alpha: Optional[torch.Tensor] = None,
-                     inv_alpha: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     inv_alpha: Optional[torch.Tensor] = None,
+                     out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                     want_raw: bool = True):
+    """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d."""
     _chk(x, "x"); dev = x.device
     for t, n in ((w_packed, "w_packed"), (bias, "bias"), (alpha, "alpha"), (inv_alpha, "inv_alpha")):
         _chk(t, n, device=dev)
     B, cin, tin = x.shape
     p = (stride + 1) // 2
     tout = (tin - 1) * stride - 2 * p + 2 * stride
-    y = torch.empty((B, cout, tout), device=dev, dtype=torch.float32)
+    ao, io, ys = _out_snake(out_snake, (B, cout, tout), dev)
+    y = torch.empty((B, cout, tout), device=dev, dtype=torch.float32) \
+        if (want_raw or out_snake is None) else None
     _lib.call("vrvq_conv_transpose1d", _p(x), B, cin, tin, _p(alpha), _p(inv_alpha),
-              _p(w_packed), cout, cout_pad, stride, _p(bias), _p(y), _stream(x))
-    return y
+              _p(w_packed), cout, cout_pad, stride, _p(bias), _p(y), _p(ao), _p(io), _p(ys),
+              _stream(x))
+    return y if out_snake is None else (y, ys)
 
 
 # ----------------------------------------------------------------------------- RVQ
