@@ -9,9 +9,9 @@
 Multi-GPU: clips shard data-parallel (each rank its own 32 clips, no data-path collective),
 weak scaling; the timed region is bracketed by barrier + synchronize and the MAX over ranks is
 reported. Rank 0 prints one JSON line, including
-  roofline      the RVQ path (rvq_codes + rvq_expand) against HBM, bytes per SURVEY.md §8(d),
-                per-launch durations from HIP events recorded on the launch stream inside the
-                timed steps;
+  roofline      the single-launch RVQ kernel (vrvq_rvq_fused: residual chain + z_q_is stream +
+                importance gating) against HBM, bytes per SURVEY.md §8(d), per-launch
+                durations from HIP events recorded on the launch stream inside the timed steps;
   roofline_conv the fp32-MFMA conv stacks against the fp32 matrix peak;
   cpu_baseline  the CPU oracle (numpy, oracle/vrvq_oracle.py) timed on this host on a bounded
                 sample (rank 0, N=1 only).
@@ -38,7 +38,7 @@ SR = 44100
 
 
 def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024) -> int:
-    """Algorithmic HBM bytes of the RVQ path per launch pair:
+    """Algorithmic HBM bytes of one RVQ launch:
     per frame z read, imp read, z_q_is + z_q writes, codes (int64), latents, mask, loss;
     plus the stage weights (normalised codebook counted once more)."""
     per_frame = D * 4 + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
@@ -94,7 +94,10 @@ def conv_flops(model, B: int, L: int) -> float:
 
 
 class RvqTimer:
-    """HIP-event timing of the RVQ launches, recorded on the stream they run on."""
+    """HIP-event timing of the RVQ launch (vrvq_rvq_fused), recorded on the stream it runs
+    on."""
+
+    KERNELS = ("fused",)
 
     def __init__(self):
         self.events = []
@@ -108,34 +111,30 @@ class RvqTimer:
 
     def durations_ms(self):
         torch.cuda.synchronize()
-        out = {"codes": [], "expand": []}
+        out = {k: [] for k in self.KERNELS}
         ev = self.events
         for (t0, e0), (t1, e1) in zip(ev, ev[1:]):
-            if t0 == "codes_begin" and t1 == "codes_end":
-                out["codes"].append(e0.elapsed_time(e1))
-            if t0 == "expand_begin" and t1 == "expand_end":
-                out["expand"].append(e0.elapsed_time(e1))
+            for k in self.KERNELS:
+                if t0 == k + "_begin" and t1 == k + "_end":
+                    out[k].append(e0.elapsed_time(e1))
         return out
 
 
 def install_rvq_timer(timer: RvqTimer):
     from vrvq_amd import ops
 
-    orig_codes, orig_expand = ops.rvq_codes, ops.rvq_expand
+    def wrap(name):
+        orig = getattr(ops, "rvq_" + name)
 
-    def codes(*a, **k):
-        timer.mark("codes_begin")
-        r = orig_codes(*a, **k)
-        timer.mark("codes_end")
-        return r
+        def f(*a, **k):
+            timer.mark(name + "_begin")
+            r = orig(*a, **k)
+            timer.mark(name + "_end")
+            return r
+        setattr(ops, "rvq_" + name, f)
 
-    def expand(*a, **k):
-        timer.mark("expand_begin")
-        r = orig_expand(*a, **k)
-        timer.mark("expand_end")
-        return r
-
-    ops.rvq_codes, ops.rvq_expand = codes, expand
+    for k in RvqTimer.KERNELS:
+        wrap(k)
 
 
 def cpu_baseline(kwargs, clips: int):
@@ -226,9 +225,8 @@ def main():
     durs = timer.durations_ms()
     T = out["codes"].shape[-1]
     byt = rvq_bytes(args.batch, T, args.n_codebooks)
-    codes_ms = float(np.mean(durs["codes"])) if durs["codes"] else float("nan")
-    exp_ms = float(np.mean(durs["expand"])) if durs["expand"] else float("nan")
-    rvq_ms = codes_ms + exp_ms
+    per = {k: (float(np.mean(v)) if v else float("nan")) for k, v in durs.items()}
+    rvq_ms = sum(per.values())
     achieved = byt / (rvq_ms * 1e-3) / 1e9
     flops = conv_flops(model, args.batch, 44544)
     # conv time per step = step time minus the RVQ launches (upper bound on conv kernel time)
@@ -256,9 +254,10 @@ def main():
                        "parallelism": f"dp{world} (replicas, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "rvq_codes_kernel + rvq_expand_kernel",
-                         "bytes_per_launch": byt, "codes_us": round(codes_ms * 1e3, 2),
-                         "expand_us": round(exp_ms * 1e3, 2)},
+                         "traffic": None,
+                         "kernel": "rvq_fused_kernel (residual chain + z_q_is stream + gating)",
+                         "bytes_per_launch": byt, "path_us": round(rvq_ms * 1e3, 2),
+                         "launch_us": {k: round(v * 1e3, 2) for k, v in per.items()}},
             "roofline_conv": {"bound": "mfma", "achieved": round(conv_tflops, 2),
                               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4),

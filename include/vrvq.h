@@ -146,6 +146,49 @@ int vrvq_rvq_codes(const float* z, int batch, int dim, int frames, int nq, int n
                    int64_t* codes, float* latents, float* loss_pf, float* zst,
                    vrvq_stream_t stream);
 
+/* Projected chain (the production RVQ path: vrvq_rvq_project -> vrvq_rvq_chain ->
+ * vrvq_rvq_expand). By linearity of in_proj / out_proj, stage i's projection of the residual
+ * (models/quantize.py:353-365) is
+ *   z_e(i) = ((P_i + b_in[i]) - Qb_i) - sum_{j<i} M_ij zst_j,
+ *   P_i = W_in[i] z,  M_ij = W_in[i] W_out[j] (8x8),  Qb_i = W_in[i] sum_{j<i} b_out[j],
+ * so the chain runs in the 8-dim latent space; z_q_is / z_q come from vrvq_rvq_expand with the
+ * reference's own out_proj expression. */
+
+/* Once per weight version: mcol [nq][nq][d][d] with mcol[j][i] = M_ij for i > j (else 0) and
+ * qb [nq][d]. Supported: D == 1024, d == 8. */
+int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_out, int nq,
+                        int dim, int cdim, float* mcol, float* qb, vrvq_stream_t stream);
+
+/* P partial sums over 8 channel splits: part [8][B*T][nq*d], part[s][b*T+t][i*d+k] =
+ * sum_{c in split s} W_in[i][k][c] z[b][c][t] (in_proj without bias, all stages at once). */
+int vrvq_rvq_project(const float* z, int batch, int dim, int frames, int nq, int cdim,
+                     const float* w_in_t, float* part, vrvq_stream_t stream);
+
+/* The 8-dim chain over all nq stages (P = sum of the 8 partials in split order). Outputs as
+ * vrvq_rvq_codes (codes, latents = z_e, loss_pf, zst) plus mask [B][nq][T] (or NULL) from
+ * imp / level as in vrvq_rvq_expand. Supported: d == 8, nq <= 32, N % 256 == 0, N <= 1024. */
+int vrvq_rvq_chain(const float* part, int batch, int frames, int nq, int ncode, int cdim,
+                   const float* b_in, const float* qb, const float* mcol, const float* cb,
+                   const float* cbn, const float* c2, const float* imp, float level,
+                   int64_t* codes, float* latents, float* loss_pf, float* zst, float* mask,
+                   vrvq_stream_t stream);
+
+/* Single launch (vrvq_rvq_fused): stage 1 + stage 2 in one kernel — the residual chain above,
+ * plus, per stage, z_q_is[b,i,:,t] (the chain's own out_proj value, streamed to HBM as it is
+ * produced), the importance mask and the masked sum z_q of vrvq_rvq_expand below. Outputs are
+ * bit-identical to vrvq_rvq_codes + vrvq_rvq_expand except for the in_proj partial-sum order.
+ * Replaces VBRResidualVectorQuantize.forward's quantizer loop and masking
+ * (models/quantize.py:353-365, 389-421) and ResidualVectorQuantize.forward (:136-214, eval).
+ *   imp     [B][T] importance map or NULL (CBR: mask = 1); level as in vrvq_rvq_expand
+ *   z_q_is  [B][nq][D][T] or NULL (not materialised); mask [B][nq][T] or NULL
+ *   codes, latents, loss_pf as in vrvq_rvq_codes; z_q [B][D][T]
+ * Supported: D == 1024, d == 8, N % 256 == 0 and N <= 1024, D*T < 2^32. */
+int vrvq_rvq_fused(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
+                   const float* w_in_t, const float* b_in, const float* cb, const float* cbn,
+                   const float* c2, const float* w_out, const float* b_out, const float* imp,
+                   float level, int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
+                   float* z_q, float* mask, vrvq_stream_t stream);
+
 /* Stage 2 (vrvq_rvq_expand): HBM-streaming expansion + importance gating.
  *   z_q_is[b,i,:,t] = W_out[i] zst[b,i,t] + b_out[i]          (bit-identical to stage 1)
  *   s[b,t]          = (imp[b,t] * level) * nq                 (models/quantize.py:389)

@@ -304,3 +304,107 @@ def test_cbr_mode_of_vbr_model(manifest):
         assert out["imp_map"] is None and torch.all(out["mask_imp"] == 1)
         with pytest.raises(RuntimeError):
             model.encode(x, n_quantizers=4)
+
+
+# ------------------------------------------------------------------ single-launch RVQ kernel
+def _rvq_fp64_reference(z, st, imp, level):
+    """Plain PyTorch fp64 restatement of the RVQ chain + gating (models/quantize.py:42-103,
+    353-421; models/utils.py:55-61) on the kernels' stacked weights."""
+    z = z.double().cpu()
+    w_in_t, b_in, cb, w_out, b_out = (x.double().cpu() for x in
+                                      (st.w_in_t, st.b_in, st.cb, st.w_out, st.b_out))
+    nq = cb.shape[0]
+    B, D, T = z.shape
+    r = z.clone()
+    codes, z_q_is = [], []
+    for i in range(nq):
+        ze = torch.einsum("dk,bdt->bkt", w_in_t[i], r) + b_in[i][None, :, None]
+        e = F.normalize(ze, dim=1)
+        cn = F.normalize(cb[i], dim=1)
+        dist = (e * e).sum(1, keepdim=True) - 2 * torch.einsum("bkt,nk->bnt", e, cn) + \
+            (cn * cn).sum(1)[None, :, None]
+        idx = dist.argmin(1)
+        zq = cb[i][idx].permute(0, 2, 1)
+        q = torch.einsum("dk,bkt->bdt", w_out[i], zq) + b_out[i][None, :, None]
+        r = r - q
+        codes.append(idx)
+        z_q_is.append(q)
+    codes = torch.stack(codes, 1)
+    z_q_is = torch.stack(z_q_is, 1)
+    if imp is None:
+        mask = torch.ones(B, nq, T, dtype=torch.float64)
+    else:
+        s = imp.double().cpu()[:, None, :] * level * nq
+        mask = (s - torch.arange(nq, dtype=torch.float64)[None, :, None] >= 0).double()
+    z_q = (z_q_is * mask[:, :, None, :]).sum(1)
+    return codes, z_q_is, z_q, mask
+
+
+@pytest.mark.parametrize("path", ["encode", "fused"])
+@pytest.mark.parametrize("nq,ncode,B,T,vbr", [
+    (8, 1024, 3, 87, True), (8, 1024, 2, 1, True), (8, 1024, 2, 13, True), (8, 1024, 1, 25, False),
+    (1, 1024, 4, 87, False), (32, 1024, 2, 87, True), (4, 256, 3, 40, True), (4, 512, 2, 87, True),
+    (4, 768, 2, 12, False), (28, 1024, 2, 70, True)])
+def test_rvq_paths_vs_fp64_and_two_kernel(path, nq, ncode, B, T, vbr):
+    """The production RVQ path (vrvq_rvq_project -> vrvq_rvq_chain -> vrvq_rvq_expand) and the
+    single-launch vrvq_rvq_fused against a torch fp64 reference and against the two-kernel
+    1024-dim chain (vrvq_rvq_codes + vrvq_rvq_expand): every codebook size variant
+    (N/256 = 1..4), frame ranges that are partial (T = 1, 13, 25, 40, 70) or exact (12),
+    nq = 1 .. 32, VBR and CBR."""
+    gen = torch.Generator().manual_seed(1000 * nq + T)
+    q = vrvq_amd.model.ResidualVectorQuantize(input_dim=1024, n_codebooks=nq, codebook_size=ncode,
+                                              codebook_dim=8)
+    with torch.no_grad():
+        for p in q.parameters():
+            p.copy_(torch.randn(p.shape, generator=gen) * (0.05 if p.ndim == 3 else 1.0))
+    q = q.to(DEV).eval()
+    st = q.stacked()
+    z = (torch.randn(B, 1024, T, generator=gen) * 0.3).to(DEV)
+    imp = torch.rand(B, T, generator=gen).to(DEV) if vbr else None
+    level = 0.75
+    if path == "encode":
+        codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=level)
+    else:
+        codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=level)
+    c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())
+    zqis2, zq2, mask2 = ops.rvq_expand(zst, st.w_out, st.b_out, imp, level)
+    torch.cuda.synchronize()
+    rc, rzqis, rzq, rmask = _rvq_fp64_reference(z, st, imp, level)
+    assert (codes.cpu() == rc).float().mean().item() == 1.0
+    assert torch.equal(codes, c2)
+    np.testing.assert_array_equal(mask.cpu().numpy(), rmask.numpy())
+    assert torch.equal(mask, mask2)
+    assert rel_err(zqis.cpu().numpy(), rzqis.numpy()) < 1e-5
+    assert rel_err(zq.cpu().numpy(), rzq.numpy()) < 1e-5
+    assert rel_err(zqis.cpu().numpy(), zqis2.cpu().numpy()) < 1e-5
+    assert rel_err(lat.cpu().numpy(), lat2.cpu().numpy()) < 1e-5
+    assert rel_err(loss.cpu().numpy(), loss2.cpu().numpy()) < 1e-4
+    # the masked sum of the path's own z_q_is, in stage order, is its z_q bit for bit
+    assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)
+
+
+@pytest.mark.parametrize("path", ["encode", "fused"])
+def test_rvq_big_batch_properties(path):
+    """BASELINE config 3 shape (B=64, 32 codebooks): two rounds of workgroups per CU."""
+    gen = torch.Generator().manual_seed(5)
+    q = vrvq_amd.model.ResidualVectorQuantize(input_dim=1024, n_codebooks=32, codebook_size=1024,
+                                              codebook_dim=8)
+    with torch.no_grad():
+        for p in q.parameters():
+            p.copy_(torch.randn(p.shape, generator=gen) * (0.05 if p.ndim == 3 else 1.0))
+    q = q.to(DEV).eval()
+    st = q.stacked()
+    z = (torch.randn(64, 1024, 87, generator=gen) * 0.3).to(DEV)
+    imp = torch.rand(64, 87, generator=gen).to(DEV)
+    if path == "encode":
+        codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=1.0)
+    else:
+        codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=1.0)
+    c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())
+    zqis2, zq2, mask2 = ops.rvq_expand(zst, st.w_out, st.b_out, imp, 1.0)
+    assert (codes == c2).float().mean().item() > 0.999
+    assert torch.equal(mask, mask2)
+    ok = (codes == c2).all(1).all(1)  # clips whose chains agree everywhere
+    assert rel_err(zqis[ok].cpu().numpy(), zqis2[ok].cpu().numpy()) < 1e-6
+    assert torch.all(mask[:, 1:] <= mask[:, :-1])
+    assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)

@@ -29,6 +29,12 @@ SIGNATURES = {
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
     "vrvq_rvq_codes": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "vrvq_rvq_expand": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
+    "vrvq_rvq_cross_prep": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "vrvq_rvq_project": [_P, _I, _I, _I, _I, _I, _P, _P, _P],
+    "vrvq_rvq_chain": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P,
+                       _P],
+    "vrvq_rvq_fused": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P,
+                       _P, _P, _P, _P],
     "vrvq_masked_loss": [_P, _P, _I, _I, _I, _P, _P],
     "vrvq_mask_hard": [_P, _I, _I, _I, _P, _P],
     "vrvq_scale_imp": [_P, _I, _F, _F, _P, _P],

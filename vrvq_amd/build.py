@@ -15,8 +15,9 @@ LIB = os.path.join(HERE, "libvrvq_hip.so")
 ARCH = os.environ.get("VRVQ_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs independent fp32 chains into v_pk_* with extra
 # v_mov shuffles and +40 VGPRs in the RVQ kernel; packed math is written explicitly instead.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+OBJ_DIR = os.path.join(HERE, "build")
 
 
 def sources():
@@ -42,26 +43,42 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build vrvq_amd)")
 
 
+def _compile_and_link(out: str, extra, verbose: bool, tag: str) -> str:
+    """One hipcc process per translation unit (they compile in parallel), then one link."""
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    procs, objs = [], []
+    headers = [d for d in deps() if not d.endswith(".hip")]
+    for src in sources():
+        obj = os.path.join(OBJ_DIR, os.path.basename(src)[:-4] + tag + ".o")
+        objs.append(obj)
+        if os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj)
+                                       for d in headers + [src]):
+            continue  # object newer than its source and every header
+        cmd = [hipcc()] + FLAGS + list(extra) + ["-I", os.path.join(REPO, "include"), "-c", src,
+                                                 "-o", obj]
+        if verbose:
+            print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), cmd))
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    tmp = out + ".tmp"
+    subprocess.run([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs,
+                   check=True)
+    os.replace(tmp, out)
+    return out
+
+
 def build_library(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-I", os.path.join(REPO, "include"), "-o", tmp] + sources()
-    if verbose:
-        print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    return _compile_and_link(LIB, [], verbose, "")
 
 
 def build_stamped(verbose: bool = True) -> str:
     """Diagnostic build with in-kernel s_memtime stamps (tools/rvq_stamps.py)."""
-    out = os.path.join(HERE, "libvrvq_hip_stamps.so")
-    cmd = [hipcc()] + FLAGS + ["-DVRVQ_STAMPS", "-I", os.path.join(REPO, "include"), "-o", out] + sources()
-    if verbose:
-        print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    return out
+    return _compile_and_link(os.path.join(HERE, "libvrvq_hip_stamps.so"), ["-DVRVQ_STAMPS"],
+                             verbose, "_stamps")
 
 
 if __name__ == "__main__":

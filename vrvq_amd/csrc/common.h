@@ -16,6 +16,9 @@ static inline int vrvq_launch_status() {
   return e == hipSuccess ? 0 : (int)e;
 }
 
+// Diagnostic stamp buffer (vrvq_debug_set_stamps; written only by -DVRVQ_STAMPS builds).
+extern unsigned long long* vrvq_g_stamps;
+
 static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Snake activation, models/layers.py:30: x + (alpha + 1e-9)^-1 * sin(alpha * x)^2.
@@ -46,3 +49,21 @@ __device__ __forceinline__ float out_proj1(const float4& w0, const float4& w1, f
                                            const float4& z0, const float4& z1) {
   return dot8(w0, w1, z0, z1) + bias;
 }
+
+// LDS-DMA of `nchunks` 1-KiB chunks src -> dst (global_load_lds_dwordx4, 16 B per lane), chunk
+// q issued by wave q % nwaves (the calling wave is `wave`). Written as inline asm on purpose:
+// the compiler's own LDS-DMA tracking turns later LDS accesses it cannot disambiguate (and
+// LDS fences) into vmcnt(0) waits, i.e. it would drain unrelated stores / prefetches. Callers
+// wait for completion explicitly (s_waitcnt vmcnt) before the barrier that publishes the data.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; the callers do not use it
+__device__ __forceinline__ void vrvq_dma_chunks(const float* src, float* dst, int nchunks,
+                                                int wave, int nwaves, int lane) {
+  for (int q = wave; q < nchunks; q += nwaves) {
+    const float* gp = src + q * 256 + lane * 4;
+    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) float*)(dst + q * 256);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                 :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gp) : "memory", "m0");
+  }
+}
+#pragma clang diagnostic pop

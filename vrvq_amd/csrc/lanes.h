@@ -199,4 +199,50 @@ __device__ __forceinline__ void argmin_scatter4(float (&d)[4], int (&ix)[4], int
   amin(d[0], ix[0], xchg<8>(d[0], lane), xchg<8>(ix[0], lane));
 }
 
+// Argmin-reduce-scatter of 16 (dist, index) pairs over the wave: afterwards the 4 lanes
+// 4f .. 4f+3 hold the wave-wide argmin of frame f (smaller distance, lower index on ties).
+// Every level's exchanges are independent (ILP 8, 4, 2, 1, then two 1-wide all-reduce steps).
+__device__ __forceinline__ void argmin_scatter16(float (&d)[16], int (&ix)[16], int lane) {
+  {  // H = 32: frames 0-7 stay in the lower half, 8-15 in the upper
+    const unsigned up = (lane & 32) ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float kd = bsel(up, d[q + 8], d[q]), sd = bsel(up, d[q], d[q + 8]);
+      const int ki = bsel(up, ix[q + 8], ix[q]), si = bsel(up, ix[q], ix[q + 8]);
+      d[q] = kd; ix[q] = ki;
+      amin(d[q], ix[q], xchg<32>(sd, lane), xchg<32>(si, lane));
+    }
+  }
+  {  // H = 16
+    const unsigned up = (lane & 16) ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float kd = bsel(up, d[q + 4], d[q]), sd = bsel(up, d[q], d[q + 4]);
+      const int ki = bsel(up, ix[q + 4], ix[q]), si = bsel(up, ix[q], ix[q + 4]);
+      d[q] = kd; ix[q] = ki;
+      amin(d[q], ix[q], xchg<16>(sd, lane), xchg<16>(si, lane));
+    }
+  }
+  {  // H = 8
+    const unsigned up = (lane & 8) ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float kd = bsel(up, d[q + 2], d[q]), sd = bsel(up, d[q], d[q + 2]);
+      const int ki = bsel(up, ix[q + 2], ix[q]), si = bsel(up, ix[q], ix[q + 2]);
+      d[q] = kd; ix[q] = ki;
+      amin(d[q], ix[q], xchg<8>(sd, lane), xchg<8>(si, lane));
+    }
+  }
+  {  // H = 4 (half-row mirror partner: lane i <-> 7-i, the upper lanes have bit 2 set)
+    const unsigned up = (lane & 4) ? 0xffffffffu : 0u;
+    const float kd = bsel(up, d[1], d[0]), sd = bsel(up, d[0], d[1]);
+    const int ki = bsel(up, ix[1], ix[0]), si = bsel(up, ix[0], ix[1]);
+    d[0] = kd; ix[0] = ki;
+    amin(d[0], ix[0], xchg<4>(sd, lane), xchg<4>(si, lane));
+  }
+  // all-reduce inside each quad
+  amin(d[0], ix[0], xchg<1>(d[0], lane), xchg<1>(ix[0], lane));
+  amin(d[0], ix[0], xchg<2>(d[0], lane), xchg<2>(ix[0], lane));
+}
+
 }  // namespace vrvq

@@ -432,11 +432,11 @@ __global__ __launch_bounds__(EXP_THREADS) void rvq_expand_kernel(
 
 }  // namespace
 
-static unsigned long long* g_stamps = nullptr;
+unsigned long long* vrvq_g_stamps = nullptr;  // shared with rvq_fused.hip (common.h)
 
 // Diagnostic hook (stamped builds only): per-block per-stage s_memtime stamps of the codes kernel.
 extern "C" int vrvq_debug_set_stamps(unsigned long long* buf) {
-  g_stamps = buf;
+  vrvq_g_stamps = buf;
   return 0;
 }
 
@@ -452,7 +452,7 @@ extern "C" int vrvq_rvq_codes(const float* z, int batch, int dim, int frames, in
       ncode > 1024)
     return VRVQ_ERR_UNSUPPORTED;
   CodesArgs a{z, batch, frames, nq, ncode, w_in_t, b_in, cb, cbn, c2, w_out, b_out,
-              codes, latents, loss_pf, zst, g_stamps};
+              codes, latents, loss_pf, zst, vrvq_g_stamps};
   // Frame groups per workgroup: aim at one workgroup per CU (256 CUs), at most 3 groups
   // (768 threads, 3 waves/SIMD).
   const long long nf = (long long)batch * frames;

@@ -197,6 +197,90 @@ def rvq_expand(zst, w_out, b_out, imp=None, level: float = 1.0, want_z_q_is: boo
     return z_q_is, z_q, mask
 
 
+def rvq_cross_prep(w_in_t, w_out, b_out):
+    """M_ij = W_in[i] W_out[j] blocks (mcol [nq][nq][8][8]) and Qb [nq][8] of the projected
+    chain (once per weight version)."""
+    _chk(w_in_t, "w_in_t"); dev = w_in_t.device
+    _chk(w_out, "w_out", device=dev); _chk(b_out, "b_out", device=dev)
+    nq, D, d = w_in_t.shape
+    mcol = torch.empty((nq, nq, d, d), device=dev, dtype=torch.float32)
+    qb = torch.empty((nq, d), device=dev, dtype=torch.float32)
+    _lib.call("vrvq_rvq_cross_prep", _p(w_in_t), _p(w_out), _p(b_out), nq, D, d, _p(mcol),
+              _p(qb), _stream(w_in_t))
+    return mcol, qb
+
+
+def rvq_project(z, w_in_t):
+    """in_proj of every stage over z, as 8 channel-split partials [8, B*T, nq*8]."""
+    _chk(z, "z"); dev = z.device
+    _chk(w_in_t, "w_in_t", device=dev)
+    B, D, T = z.shape
+    nq, _, d = w_in_t.shape
+    part = torch.empty((8, B * T, nq * d), device=dev, dtype=torch.float32)
+    _lib.call("vrvq_rvq_project", _p(z), B, D, T, nq, d, _p(w_in_t), _p(part), _stream(z))
+    return part
+
+
+def rvq_chain(part, B, T, b_in, qb, mcol, cb, cbn, c2, imp=None, level: float = 1.0,
+              want_mask: bool = True):
+    """8-dim residual chain: codes, latents, loss_pf, zst, mask (see include/vrvq.h)."""
+    _chk(part, "part"); dev = part.device
+    for t_, n_ in ((b_in, "b_in"), (qb, "qb"), (mcol, "mcol"), (cb, "cb"), (cbn, "cbn"),
+                   (c2, "c2")):
+        _chk(t_, n_, device=dev)
+    _chk(imp, "imp", device=dev)
+    nq, N, d = cb.shape
+    codes = torch.empty((B, nq, T), device=dev, dtype=torch.int64)
+    latents = torch.empty((B, nq * d, T), device=dev, dtype=torch.float32)
+    loss_pf = torch.empty((B, nq, T), device=dev, dtype=torch.float32)
+    zst = torch.empty((B, nq, T, d), device=dev, dtype=torch.float32)
+    mask = torch.empty((B, nq, T), device=dev, dtype=torch.float32) if want_mask else None
+    _lib.call("vrvq_rvq_chain", _p(part), B, T, nq, N, d, _p(b_in), _p(qb), _p(mcol), _p(cb),
+              _p(cbn), _p(c2), _p(imp), float(level), _p(codes), _p(latents), _p(loss_pf),
+              _p(zst), _p(mask), _stream(part))
+    return codes, latents, loss_pf, zst, mask
+
+
+def rvq_encode(z, st, imp=None, level: float = 1.0, want_z_q_is: bool = True,
+               want_mask: bool = True):
+    """The production RVQ path: projection GEMM -> 8-dim chain -> HBM expansion (three
+    launches). `st` is a model._Stacked (folded, stacked stage weights + cross terms).
+    Returns codes, latents, loss_pf, z_q_is (or None), z_q, mask (or None)."""
+    B, D, T = z.shape
+    part = rvq_project(z, st.w_in_t)
+    codes, latents, loss_pf, zst, mask = rvq_chain(part, B, T, st.b_in, st.qb, st.mcol, st.cb,
+                                                   st.cbn, st.c2, imp, level, want_mask)
+    z_q_is, z_q, _ = rvq_expand(zst, st.w_out, st.b_out, imp, level, want_z_q_is=want_z_q_is,
+                                want_mask=False)
+    return codes, latents, loss_pf, z_q_is, z_q, mask
+
+
+def rvq_fused(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp=None, level: float = 1.0,
+              want_z_q_is: bool = True, want_mask: bool = True):
+    """Residual chain + z_q_is stream + importance gating in one launch (vrvq_rvq_fused).
+
+    Returns codes int64 [B,nq,T], latents [B,nq*d,T], loss_pf [B,nq,T], z_q_is [B,nq,D,T] (or
+    None), z_q [B,D,T], mask [B,nq,T] (or None).
+    """
+    _chk(z, "z"); dev = z.device
+    for t, n in ((w_in_t, "w_in_t"), (b_in, "b_in"), (cb, "cb"), (cbn, "cbn"), (c2, "c2"),
+                 (w_out, "w_out"), (b_out, "b_out")):
+        _chk(t, n, device=dev)
+    _chk(imp, "imp", device=dev)
+    B, D, T = z.shape
+    nq, N, d = cb.shape
+    codes = torch.empty((B, nq, T), device=dev, dtype=torch.int64)
+    latents = torch.empty((B, nq * d, T), device=dev, dtype=torch.float32)
+    loss_pf = torch.empty((B, nq, T), device=dev, dtype=torch.float32)
+    z_q_is = torch.empty((B, nq, D, T), device=dev, dtype=torch.float32) if want_z_q_is else None
+    z_q = torch.empty((B, D, T), device=dev, dtype=torch.float32)
+    mask = torch.empty((B, nq, T), device=dev, dtype=torch.float32) if want_mask else None
+    _lib.call("vrvq_rvq_fused", _p(z), B, D, T, nq, N, d, _p(w_in_t), _p(b_in), _p(cb), _p(cbn),
+              _p(c2), _p(w_out), _p(b_out), _p(imp), float(level), _p(codes), _p(latents),
+              _p(loss_pf), _p(z_q_is), _p(z_q), _p(mask), _stream(z))
+    return codes, latents, loss_pf, z_q_is, z_q, mask
+
+
 def masked_loss(loss_pf: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
     _chk(loss_pf, "loss_pf"); _chk(mask, "mask", device=loss_pf.device)
     B, nq, T = loss_pf.shape
