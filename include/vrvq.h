@@ -98,6 +98,19 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
 int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
                             float* w_packed, vrvq_stream_t stream);
 
+/* Fused ResidualUnit (models/layers.py:52-68), stride 1, k = 7 then k = 1, C channels:
+ *   y = x + b1 + W1 * snake2(b7 + W7 *_dil x_snk),   x_snk = snake1(x) (given)
+ * with y and / or y_snake = snake_out(y) written (as vrvq_conv1d's out_snake). The
+ * intermediate snake2(...) stays in LDS. Bit-identical to vrvq_conv1d(k7, out_snake = snake2,
+ * no raw) followed by vrvq_conv1d(k1, residual = x). w7_packed / w1_packed as packed by
+ * vrvq_pack_conv1d_weight (same cout_pad). Supported: C in {64, 96, 128, 192}, dil <= 9;
+ * other C return VRVQ_ERR_UNSUPPORTED (callers use the two-launch form). */
+int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels, int frames,
+                       int dil, const float* w7_packed, const float* b7, const float* alpha2,
+                       const float* inv_alpha2, const float* w1_packed, const float* b1,
+                       int cout_pad, float* y, const float* alpha_out,
+                       const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
+
 /* Snake-fused ConvTranspose1d, kernel = 2*stride, padding = stride/2 (even stride), i.e.
  * the DecoderBlock upsampler (models/layers.py:92-103): y has length tin*stride.
  * Computed as a polyphase 2-tap conv with cout*stride phase-channels:

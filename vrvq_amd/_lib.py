@@ -25,6 +25,8 @@ SIGNATURES = {
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
+    "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P,
+                           _P],
     "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
     "vrvq_rvq_codes": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],

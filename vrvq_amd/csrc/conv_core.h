@@ -1,0 +1,384 @@
+// Shared building blocks of the MFMA implicit-GEMM convolutions (conv.hip) and the fused
+// ResidualUnit (conv_ru.hip): argument block, tile configuration, the K-chunk mainloop and the
+// LDS-transposed epilogue. See conv.hip for the GEMM mapping and the MFMA operand layouts.
+#pragma once
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace vrvq_conv {
+
+struct ConvArgs {
+  const float* x;          // [B][cin][tin]
+  const float* alpha;      // [cin] or null
+  const float* inv_alpha;  // [cin]
+  const float* w;          // [cin][KS][m_pad]
+  const float* bias;       // [cout] or null
+  const float* res;        // [B][cout][ylen] or null
+  float* y;                // [B][cout][ylen] or null
+  const float* alpha_o;    // [cout] snake of the NEXT layer, applied in the epilogue, or null
+  const float* inv_alpha_o;
+  float* ys;               // [B][cout][ylen] snake_o(y), or null
+  int cin, tin;
+  int M;                   // GEMM rows: cout (normal) or cout*up (transposed)
+  int m_pad;
+  int cout;
+  int stride, pad, dil;
+  int ssh;                 // log2(stride) for a power-of-two stride >= 2 (phase-split window), else 0
+  int ng;                  // GEMM columns (output positions of the GEMM)
+  int up, up_pad;          // transposed conv: upsample factor and its padding (0 = normal)
+  int ylen;                // output row length
+  int epi;
+  int n_mt, n_nt;          // M tiles, N tiles
+};
+
+template <int KS, int BM>
+struct ChunkCfg {
+  // Input channels per K-chunk: CK*KS ~ 32..64 rows of W per stage (half for 192-row tiles,
+  // so two double-buffered stages still fit twice per CU).
+  static constexpr int CK0 = KS == 1 ? 32 : KS <= 4 ? 16 : KS <= 8 ? 8 : 4;
+  static constexpr int CK = (BM > 128 && CK0 >= 8) ? CK0 / 2 : CK0;
+};
+
+__device__ __forceinline__ float apply_epi(float v, int epi) {
+  if (epi == VRVQ_EPI_TANH) return tanhf(v);
+  if (epi == VRVQ_EPI_SIGMOID) return 1.0f / (1.0f + expf(-v));
+  return v;
+}
+
+// Largest input window a thread stages per K-chunk: stride <= KS/2 for the strided (k = 2s)
+// encoder convs, dilation <= 9 for the k = 7 residual-unit convs.
+template <int KS, int BN>
+struct WinCfg {
+  static constexpr int SMAX = (KS == 4 || KS == 8 || KS == 16) ? KS / 2 : 1;
+  static constexpr int DMAX = KS == 7 ? 9 : 1;
+  static constexpr int XW_MAX = (BN - 1) * SMAX + (KS - 1) * DMAX + 1;
+  static constexpr int PER_ROW = (XW_MAX + 63) / 64;  // positions per lane per row
+};
+
+// Epilogue column passes: the accumulator tile goes through LDS in BM x (BN / EPASS) pieces of
+// at most 64 KiB, EPASS dividing the wave-column count.
+template <int BM, int BN, int WN>
+struct EpiCfg {
+  static constexpr int need = (BM * BN * 4 + 65535) / 65536;
+  static constexpr int EPASS = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+  static_assert(WN % EPASS == 0 || EPASS == 1, "epilogue passes must split the wave columns");
+  static constexpr int BNP = BN / EPASS;
+};
+
+
+// Tile geometry shared by the mainloop / epilogue of one <BM, BN, WM, NW> configuration.
+template <int BM, int BN, int WM, int NW>
+struct TileCfg {
+  static constexpr int NT = 64 * NW;
+  static constexpr int WN = NW / WM;
+  static constexpr int TM = BM / WM;
+  static constexpr int TN = BN / WN;
+  static constexpr int RM = TM / 32;
+  static constexpr int RN = TN / 32;
+};
+
+// K loop over a.cin in chunks of CK input channels x KS taps: two LDS stages [W chunk | x
+// window], the next chunk prefetched into registers while the current one feeds the MFMAs, one
+// barrier per chunk. acc must be zero on entry. Ends with a barrier (every stage buffer free).
+template <int BM, int BN, int WM, int NW, int KS>
+__device__ __forceinline__ void conv_mainloop(
+    const ConvArgs& a, float* smem,
+    f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
+    int n0) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = NW / WM;
+  constexpr int TM = BM / WM;
+  constexpr int TN = BN / WN;
+  constexpr int RM = TM / 32;
+  constexpr int RN = TN / 32;
+  constexpr int CK = ChunkCfg<KS, BM>::CK;
+  constexpr int KROWS = CK * KS;
+  constexpr int WQ4 = KROWS * BM / 4;               // float4 of W per chunk
+  constexpr int WQ = (WQ4 + NT - 1) / NT;           // ... per thread
+  constexpr int XROWS = (CK + NW - 1) / NW;         // x rows per wave per chunk
+  constexpr int XPR = WinCfg<KS, BN>::PER_ROW;
+  static_assert(NW * 64 == NT && WM * WN == NW, "waves");
+  static_assert(RM >= 1 && RN >= 1 && TM % 32 == 0 && TN % 32 == 0, "tile");
+  static_assert(CK % 2 == 0, "chunk shape");
+
+  const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
+  const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
+  const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
+  const int STG = KROWS * BM + CK * XWP;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int lr = lane & 31;
+  const int lh = lane >> 5;
+
+  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  const int xbase = n0 * a.stride - a.pad;
+  // Wave-uniform fast paths: every chunk holds CK real channels, and the window lies inside
+  // [0, tin) (no zero padding): the loads then need no per-lane predicates.
+  const bool cin_full = a.cin % CK == 0;
+  const bool interior = cin_full && xbase >= 0 && xbase + XW <= a.tin;
+
+  float4 wreg[WQ];
+  float xreg[XROWS][XPR];
+
+  auto load_chunk = [&](int ci0) {
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int idx = tid + q * NT;
+      const int rr = idx / (BM / 4);
+      const int cc = (idx - rr * (BM / 4)) * 4;
+      const float4* src = reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc);
+      if (WQ4 % NT == 0 && cin_full) wreg[q] = *src;
+      else wreg[q] = (idx < WQ4 && ci0 + rr / KS < a.cin) ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (interior) {
+#pragma unroll
+      for (int rw = 0; rw < XROWS; ++rw) {
+        const int cl = wave + NW * rw;
+        const float* xr = xb + (size_t)(ci0 + cl) * a.tin + xbase;
+#pragma unroll
+        for (int u = 0; u < XPR; ++u) {
+          const int p = lane + 64 * u;
+          xreg[rw][u] = (cl < CK && p < XW) ? xr[p] : 0.0f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int rw = 0; rw < XROWS; ++rw) {
+        const int cl = wave + NW * rw;
+        const int ci = ci0 + cl;
+        const float* xr = xb + (size_t)ci * a.tin;
+#pragma unroll
+        for (int u = 0; u < XPR; ++u) {
+          const int p = lane + 64 * u;
+          const int t = xbase + p;
+          xreg[rw][u] = (cl < CK && ci < a.cin && p < XW && t >= 0 && t < a.tin) ? xr[t] : 0.0f;
+        }
+      }
+    }
+  };
+  auto store_chunk = [&](float* stg, int ci0) {
+    float* ws = stg;
+    float* xs = stg + KROWS * BM;
+#pragma unroll
+    for (int q = 0; q < WQ; ++q)
+      if (WQ4 % NT == 0 || tid + q * NT < WQ4) reinterpret_cast<float4*>(ws)[tid + q * NT] = wreg[q];
+#pragma unroll
+    for (int rw = 0; rw < XROWS; ++rw) {
+      const int cl = wave + NW * rw;
+      if (cl >= CK) continue;
+      const int ci = ci0 + cl;
+      const bool sn = a.alpha != nullptr && ci < a.cin;
+      const float al = sn ? a.alpha[ci] : 0.f, ia = sn ? a.inv_alpha[ci] : 0.f;
+#pragma unroll
+      for (int u = 0; u < XPR; ++u) {
+        const int p = lane + 64 * u;
+        float v = xreg[rw][u];
+        if (sn) v = snake_act(v, al, ia);  // snake(0) = 0: zero padding commutes with Snake
+        if (a.ssh) {
+          if (p < XW) xs[cl * XWP + (p & (a.stride - 1)) * XP + (p >> a.ssh)] = v;
+        } else if (p < XWP) {
+          xs[cl * XWP + p] = v;
+        }
+      }
+    }
+  };
+
+  int cur = 0;
+  load_chunk(0);
+  store_chunk(smem, 0);
+  __syncthreads();
+  for (int ci0 = 0; ci0 < a.cin; ci0 += CK) {
+    const bool more = ci0 + CK < a.cin;
+    if (more) load_chunk(ci0 + CK);  // global loads in flight during the MFMAs below
+    const float* ws = smem + cur * STG;
+    const float* xs = ws + KROWS * BM;
+    // ---- MFMA over the chunk: K order = (tap, channel pair) ----
+    // Software-pipelined: the LDS operands of step s+1 are read before the MFMAs of step s
+    // are issued, so the ds_read latency hides behind the MFMAs instead of stalling every
+    // step on lgkmcnt(0).
+    constexpr int CP = CK / 2;
+    constexpr int NSTEP = KS * CP;
+    const int col = wn * TN + lr;
+    auto rd = [&](int st, float (&av)[RM], float (&bv)[RN]) {
+      const int k = st / CP, kr = (st % CP) * 2 + lh;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) av[i] = ws[(kr * KS + k) * BM + wm * TM + i * 32 + lr];
+      const int xo = a.ssh ? kr * XWP + (k & (a.stride - 1)) * XP + col + (k >> a.ssh)
+                           : kr * XWP + col + k * a.dil;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bv[j] = xs[xo + j * 32];
+    };
+    auto mma = [&](const float (&av)[RM], const float (&bv)[RN]) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
+    {
+      float a0[RM], b0[RN], a1[RM], b1[RN];
+      rd(0, a0, b0);
+#pragma unroll
+      for (int st = 0; st < NSTEP; st += 2) {
+        // sched_barrier(0): keep each read group ahead of the MFMAs it overlaps (the
+        // scheduler otherwise sinks the reads to the MFMAs that consume them).
+        if (st + 1 < NSTEP) rd(st + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < NSTEP) rd(st + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < NSTEP) mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (more) store_chunk(smem + (cur ^ 1) * STG, ci0 + CK);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+}
+
+// Epilogue through LDS: the accumulator tile is transposed to row-major [BM][BNP] so each wave
+// stores 64 consecutive output positions of one row (bias, residual, Tanh/Sigmoid, y and the
+// next layer's Snake). Expects every LDS buffer free (after a barrier).
+template <int BM, int BN, int WM, int NW>
+__device__ __forceinline__ void conv_epilogue(
+    const ConvArgs& a, float* smem,
+    f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
+    int n0) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = NW / WM;
+  constexpr int TM = BM / WM;
+  constexpr int TN = BN / WN;
+  constexpr int RM = TM / 32;
+  constexpr int RN = TN / 32;
+  constexpr int EPASS = EpiCfg<BM, BN, WN>::EPASS;
+  constexpr int BNP = EpiCfg<BM, BN, WN>::BNP;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int lr = lane & 31;
+  const int lh = lane >> 5;
+
+  // ---- epilogue through LDS (every stage buffer is free after the loop's last barrier) ----
+  // The accumulator tile is transposed to row-major [BM][BNP] (EPASS column passes) so that
+  // each wave then handles 64 consecutive output positions of one row: residual loads and
+  // y / snake(y) stores are 256-B coalesced, and the per-element Snake of the next layer runs
+  // in a rolled loop.
+  float* ct = smem;
+  const int mrows = min(BM, a.M - m0);
+#pragma unroll
+  for (int pass = 0; pass < EPASS; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wn / (WN / EPASS) == pass) {
+      const int cbase = wn * TN - pass * BNP;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ct[(wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * BNP + cbase + j * 32 + lr] =
+                acc[i][j][r];
+    }
+    __syncthreads();
+    const int p0 = n0 + pass * BNP;  // first GEMM column of this pass
+    if (a.up == 0) {
+      // Each thread owns 4 consecutive columns per step; U steps are loaded (accumulator
+      // tile, bias, residual, next-layer alpha) before anything is stored, so the global
+      // loads of a step group are in flight together.
+      constexpr int NV = BNP / 4;
+      constexpr int ITER = (BM * NV + NT - 1) / NT;
+      constexpr int U = ITER >= 4 ? 4 : ITER;
+      const int ncols = min(BNP, a.ng - p0);
+      const bool vec = (a.ylen & 3) == 0;
+      for (int it0 = 0; it0 < ITER; it0 += U) {
+        float v[U][4], sa[U], si[U];
+        size_t ob[U];
+        int nl[U];
+        bool ok[U], full[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = tid + NT * (it0 + u);
+          const int ml = e / NV;
+          nl[u] = (e - ml * NV) * 4;
+          ok[u] = it0 + u < ITER && ml < mrows && nl[u] < ncols;
+          full[u] = vec && nl[u] + 4 <= ncols;
+          const int m = ok[u] ? m0 + ml : m0;
+          const float4 c = ok[u] ? *reinterpret_cast<const float4*>(ct + ml * BNP + nl[u])
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float bb = (a.bias && ok[u]) ? a.bias[m] : 0.0f;
+          v[u][0] = c.x + bb; v[u][1] = c.y + bb; v[u][2] = c.z + bb; v[u][3] = c.w + bb;
+          ob[u] = ((size_t)b * a.cout + m) * a.ylen + p0 + nl[u];
+          sa[u] = (a.ys && ok[u]) ? a.alpha_o[m] : 0.0f;
+          si[u] = (a.ys && ok[u]) ? a.inv_alpha_o[m] : 0.0f;
+          if (a.res && ok[u]) {
+            if (full[u]) {
+              const float4 r = *reinterpret_cast<const float4*>(a.res + ob[u]);
+              v[u][0] = r.x + v[u][0]; v[u][1] = r.y + v[u][1];
+              v[u][2] = r.z + v[u][2]; v[u][3] = r.w + v[u][3];
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) v[u][q] = a.res[ob[u] + q] + v[u][q];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] = apply_epi(v[u][q], a.epi);
+          if (a.y && ok[u]) {
+            if (full[u]) {
+              *reinterpret_cast<float4*>(a.y + ob[u]) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) a.y[ob[u] + q] = v[u][q];
+            }
+          }
+        }
+        if (a.ys) {
+          for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            float sv[4];
+            for (int q = 0; q < 4; ++q) sv[q] = snake_act(v[u][q], sa[u], si[u]);
+            if (full[u]) {
+              *reinterpret_cast<float4*>(a.ys + ob[u]) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+            } else {
+              for (int q = 0; q < 4; ++q)
+                if (nl[u] + q < ncols) a.ys[ob[u] + q] = sv[q];
+            }
+          }
+        }
+      }
+    } else {
+      // transposed conv: GEMM row m = co*up + phase, column n -> t = n*up + phase - up_pad.
+      // Walk (channel, t) so consecutive lanes store consecutive t.
+      const int up = a.up, tl_n = BNP * up;
+      const int co0 = m0 / up, nco = min(BM / up, a.cout - co0);
+      for (int e = tid; e < BM * BNP; e += NT) {
+        const int cl = e / tl_n, tl = e - cl * tl_n;
+        const int nl = tl / up, ph = tl - nl * up;
+        const int t = (p0 + nl) * up + ph - a.up_pad;
+        if (cl < nco && p0 + nl < a.ng && t >= 0 && t < a.ylen) {
+          const int co = co0 + cl;
+          float v = ct[(cl * up + ph) * BNP + nl];
+          if (a.bias) v = v + a.bias[co];
+          const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
+          if (a.y) a.y[o] = v;
+          if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[co], a.inv_alpha_o[co]);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace vrvq_conv

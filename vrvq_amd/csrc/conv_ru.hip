@@ -1,0 +1,183 @@
+// Fused ResidualUnit for gfx950 (models/layers.py:52-68):
+//   y = x + conv1(snake2(conv7_dil(snake1(x)))),  snake1(x) given (producer-side Snake)
+// in one launch per (clip, time tile), all C channels in the workgroup:
+//   phase 1  h = W7 * window(x_snk) + b7         the conv.hip mainloop (K = 7C, MFMA)
+//   mid      hs = snake2(h) -> LDS tile [C][BN]  never written to HBM
+//   phase 2  acc = W1 * hs                        K = C; B operand straight from the LDS tile,
+//                                                 A operand (W1, L2-resident) register-
+//                                                 prefetched a group of steps ahead, no barriers
+//   out      y = acc + b1 + x (y optional) and snake_next(y)   the conv.hip epilogue
+// Versus the two-launch form this removes the write + re-read of snake2(h) (2 C*T*4 bytes per
+// unit and clip) and the separate k=1 launch. The MFMA K order of both phases and every
+// epilogue expression are those of the two launches, so the output is bit-identical to them.
+// Instantiated for C in {64, 96, 128, 192} (the long-time-axis blocks); other widths use the
+// two-launch form.
+#include "common.h"
+#include "conv_core.h"
+
+namespace {
+
+using namespace vrvq_conv;
+
+struct RuArgs {
+  ConvArgs p1;         // phase 1 (x = snake1(x), w = W7 packed, no Snake prologue)
+  ConvArgs p2;         // epilogue (bias b1, residual x, y / ys / next Snake)
+  const float* b7;     // [C]
+  const float* alpha2; // [C]  Snake between the two convs
+  const float* inv_alpha2;
+  const float* w1;     // [C][1][m_pad]  packed k=1 weight
+  int C;
+};
+
+template <int BM, int BN, int WM, int NW>
+__global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
+  using TC = TileCfg<BM, BN, WM, NW>;
+  constexpr int RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
+  constexpr int NS = BM / 2;   // phase-2 MFMA steps (k = 2 channels per step)
+  constexpr int PF = 8;        // steps per prefetch group
+  static_assert(NS % PF == 0, "phase-2 steps per group");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const ConvArgs& a = ra.p1;
+  const int nt = blockIdx.x % a.n_nt;
+  const int b = blockIdx.x / a.n_nt;
+  const int n0 = nt * BN;
+  const int C = ra.C;
+
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  conv_mainloop<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);  // ends with a barrier
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // ---- mid: hs[row][col] = snake2(h + b7) in the MFMA D layout (rows >= C: zero) ----
+  float* hs = smem;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const bool ok = row < C;
+      const float bb = ok ? ra.b7[row] : 0.0f;
+      const float al = ok ? ra.alpha2[row] : 0.0f, ia = ok ? ra.inv_alpha2[row] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const float v = acc[i][j][r] + bb;  // conv.hip epilogue: c + bias
+        hs[row * BN + wn * TN + j * 32 + lr] = ok ? snake_act(v, al, ia) : 0.0f;
+      }
+    }
+  __syncthreads();
+
+  // ---- phase 2: acc = W1 * hs over K = C in channel pairs (the k=1 launch's K order) ----
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  const float* wa = ra.w1 + (size_t)lh * a.m_pad + wm * TM + lr;  // + 2 s m_pad + i 32
+  const float* hb = hs + lh * BN + wn * TN + lr;                  // + 2 s BN + j 32
+  float an[PF][RM];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int i = 0; i < RM; ++i) an[p][i] = wa[(size_t)(2 * p) * a.m_pad + i * 32];
+  for (int g = 0; g < NS; g += PF) {
+    float ac[PF][RM];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int i = 0; i < RM; ++i) ac[p][i] = an[p][i];
+    if (g + PF < NS) {  // next group's W1 values in flight during this group's MFMAs
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int i = 0; i < RM; ++i) an[p][i] = wa[(size_t)(2 * (g + PF + p)) * a.m_pad + i * 32];
+    }
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      float bv[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bv[j] = hb[(2 * (g + p)) * BN + j * 32];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[p][i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // hs reads done: the epilogue reuses the LDS
+  conv_epilogue<BM, BN, WM, NW>(ra.p2, smem, acc, b, 0, n0);
+}
+
+template <int BM, int BN, int WM, int NW>
+int launch_ru(RuArgs ra, int batch, hipStream_t st) {
+  constexpr int CK = ChunkCfg<7, BM>::CK;
+  ConvArgs& a = ra.p1;
+  a.n_mt = 1;
+  a.n_nt = (a.ng + BN - 1) / BN;
+  ra.p2.n_mt = 1;
+  ra.p2.n_nt = a.n_nt;
+  if (a.m_pad < BM || ra.C > BM) return VRVQ_ERR_ARG;
+  const int XW = (BN - 1) + 6 * a.dil + 1;
+  const int XWP = (XW + 3) & ~3;
+  if (XW > 64 * WinCfg<7, BN>::PER_ROW) return VRVQ_ERR_UNSUPPORTED;
+  size_t lds = 2 * (size_t)(CK * 7 * BM + CK * XWP) * sizeof(float);
+  const size_t hsz = (size_t)BM * BN * sizeof(float);
+  const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
+  if (lds < hsz) lds = hsz;
+  if (lds < epi) lds = epi;
+  if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)ru_fused_kernel<BM, BN, WM, NW>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const long long nblk = (long long)a.n_nt * batch;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  hipLaunchKernelGGL((ru_fused_kernel<BM, BN, WM, NW>), dim3((unsigned)nblk), dim3(64 * NW), lds,
+                     st, ra);
+  return vrvq_launch_status();
+}
+
+}  // namespace
+
+extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels,
+                                  int frames, int dil, const float* w7_packed, const float* b7,
+                                  const float* alpha2, const float* inv_alpha2,
+                                  const float* w1_packed, const float* b1, int cout_pad,
+                                  float* y, const float* alpha_out, const float* inv_alpha_out,
+                                  float* y_snake, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && x_snk && w7_packed && b7 && alpha2 && inv_alpha2 && w1_packed && b1);
+  VRVQ_CHECK_ARG(y || y_snake);
+  VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
+  VRVQ_CHECK_ARG(batch > 0 && channels > 0 && frames > 0 && dil >= 1 && dil <= 9);
+  VRVQ_CHECK_ARG(cout_pad >= channels && cout_pad % 128 == 0);
+  RuArgs ra{};
+  ConvArgs& p = ra.p1;
+  p.x = x_snk; p.alpha = nullptr; p.inv_alpha = nullptr; p.w = w7_packed; p.bias = nullptr;
+  p.res = nullptr; p.y = nullptr; p.alpha_o = nullptr; p.inv_alpha_o = nullptr; p.ys = nullptr;
+  p.cin = channels; p.tin = frames; p.M = channels; p.m_pad = cout_pad; p.cout = channels;
+  p.stride = 1; p.pad = 3 * dil; p.dil = dil; p.ssh = 0; p.ng = frames; p.up = 0; p.up_pad = 0;
+  p.ylen = frames; p.epi = VRVQ_EPI_NONE;
+  ConvArgs& q = ra.p2;
+  q = p;
+  q.bias = b1; q.res = x; q.y = y; q.alpha_o = alpha_out; q.inv_alpha_o = inv_alpha_out;
+  q.ys = y_snake;
+  ra.b7 = b7; ra.alpha2 = alpha2; ra.inv_alpha2 = inv_alpha2; ra.w1 = w1_packed;
+  ra.C = channels;
+  hipStream_t st = as_stream(stream);
+  switch (channels) {
+    case 64: return launch_ru<64, 128, 2, 4>(ra, batch, st);
+    case 96: return launch_ru<96, 128, 1, 4>(ra, batch, st);
+    case 128: return launch_ru<128, 128, 2, 4>(ra, batch, st);
+    case 192: return launch_ru<192, 64, 2, 4>(ra, batch, st);
+    default: return VRVQ_ERR_UNSUPPORTED;
+  }
+}

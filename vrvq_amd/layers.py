@@ -150,6 +150,8 @@ class WNConvTranspose1d(nn.Module):
 class ResidualUnit(nn.Module):
     """x + conv1(snake(conv7_dil(snake(x))))  (models/layers.py:52-68)."""
 
+    fused = True  # class-level switch (tests / A-B timing): single-launch form where supported
+
     def __init__(self, dim: int = 16, dilation: int = 1):
         super().__init__()
         pad = ((7 - 1) * dilation) // 2
@@ -167,8 +169,21 @@ class ResidualUnit(nn.Module):
 
     def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool):
         """Chained form: x_snk = block[0](x) was produced by the previous layer's epilogue.
-        The k7 conv writes only block[2](h) (h has no other consumer); the k1 conv adds the
-        skip and writes (y if want_raw, out_snake(y)) for the next layer."""
+        For C in ops.RU_FUSED_CHANNELS one launch (vrvq_residual_unit: block[2](h) stays in
+        LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
+        k1 conv adds the skip. Either way the output is (y if want_raw, out_snake(y)), bit for
+        bit the same."""
+        if self.fused and x.shape[1] in ops.RU_FUSED_CHANNELS:
+            w7, cp7 = self.block[1].prepared()
+            w1, cp1 = self.block[3].prepared()
+            a2, ia2 = self.block[2].prepared()
+            return ops.residual_unit(x, x_snk, self.block[1].dilation[0], w7,
+                                     self.block[1].bias.detach(), a2, ia2, w1,
+                                     self.block[3].bias.detach(), cp7,
+                                     out_snake=out_snake.prepared(), want_raw=want_raw)
+        return self.run_two_launch(x, x_snk, out_snake, want_raw)
+
+    def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool):
         _, h_snk = self.block[1](x_snk, out_snake=self.block[2], want_raw=False)
         return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw)
 

@@ -160,6 +160,30 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
     return y if out_snake is None else (y, ys)
 
 
+RU_FUSED_CHANNELS = (64, 96, 128, 192)
+
+
+def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad: int,
+                  out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                  want_raw: bool = True):
+    """Fused ResidualUnit: x + conv1(snake2(conv7_dil(x_snk))) in one launch (include/vrvq.h,
+    vrvq_residual_unit). Returns y, or (y | None, snake_next(y)) when out_snake is given."""
+    _chk(x, "x"); dev = x.device
+    for t, n in ((x_snk, "x_snk"), (w7, "w7"), (b7, "b7"), (alpha2, "alpha2"),
+                 (inv_alpha2, "inv_alpha2"), (w1, "w1"), (b1, "b1")):
+        _chk(t, n, device=dev)
+    B, C, T = x.shape
+    if tuple(x_snk.shape) != (B, C, T):
+        raise RuntimeError("residual_unit: x_snk must have the shape of x")
+    ao, io, ys = _out_snake(out_snake, (B, C, T), dev)
+    y = torch.empty((B, C, T), device=dev, dtype=torch.float32) \
+        if (want_raw or out_snake is None) else None
+    _lib.call("vrvq_residual_unit", _p(x), _p(x_snk), B, C, T, int(dil), _p(w7), _p(b7),
+              _p(alpha2), _p(inv_alpha2), _p(w1), _p(b1), int(cout_pad), _p(y), _p(ao), _p(io),
+              _p(ys), _stream(x))
+    return y if out_snake is None else (y, ys)
+
+
 # ----------------------------------------------------------------------------- RVQ
 def rvq_codes(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out):
     """Sequential residual chain over nq = w_in_t.shape[0] stages.
