@@ -101,9 +101,10 @@ int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_p
 /* Fused ResidualUnit (models/layers.py:52-68), stride 1, k = 7 then k = 1, C channels:
  *   y = x + b1 + W1 * snake2(b7 + W7 *_dil x_snk),   x_snk = snake1(x) (given)
  * with y and / or y_snake = snake_out(y) written (as vrvq_conv1d's out_snake). The
- * intermediate snake2(...) stays in LDS. Bit-identical to vrvq_conv1d(k7, out_snake = snake2,
- * no raw) followed by vrvq_conv1d(k1, residual = x). w7_packed / w1_packed as packed by
- * vrvq_pack_conv1d_weight (same cout_pad). Supported: C in {64, 96, 128, 192}, dil <= 9;
+ * intermediate snake2(...) stays in LDS. Same expressions as vrvq_conv1d(k7, out_snake =
+ * snake2, no raw) followed by vrvq_conv1d(k1, residual = x) — bit-identical where both use the
+ * same k7 tile height (C <= 192), else the same sums in another fp32 order. Packed by
+ * vrvq_pack_conv1d_weight (same cout_pad). Supported: C in {64, 96, 128, 192, 256}, dil <= 9;
  * other C return VRVQ_ERR_UNSUPPORTED (callers use the two-launch form). */
 int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels, int frames,
                        int dil, const float* w7_packed, const float* b7, const float* alpha2,

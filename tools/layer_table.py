@@ -38,8 +38,16 @@ def _fake():
         y = torch.empty(B, cout, tin * stride)
         return y if out_snake is None else (y, torch.empty_like(y))
 
+    def residual_unit(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad,
+                      out_snake=None, want_raw=True):
+        B, C, T = x.shape
+        CALLS.append(("RU", C, C, 7, 1, dil, T, B, 2.0 * B * C * T * C * 8, True))
+        y = torch.empty(B, C, T)
+        return y if out_snake is None else (y, torch.empty_like(y))
+
     ops.conv1d = conv1d
     ops.conv_transpose1d = convt
+    ops.residual_unit = residual_unit
     ops.weight_norm = lambda g, v: v
     ops.snake_inv_alpha = lambda a: a
     ops.pack_conv1d_weight = lambda w: (w, 128)
@@ -57,8 +65,19 @@ def _fake():
         D = w_out.shape[1]
         return torch.empty(B, nq, D, T), torch.empty(B, D, T), torch.empty(B, nq, T)
 
+    def rvq_fused(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp=None, level=1.0,
+                  want_z_q_is=True, want_mask=True):
+        B, D, T = z.shape
+        nq = cb.shape[0]
+        return (torch.zeros(B, nq, T, dtype=torch.long), torch.empty(B, nq * 8, T),
+                torch.empty(B, nq, T), torch.empty(B, nq, D, T), torch.empty(B, D, T),
+                torch.empty(B, nq, T))
+
     ops.rvq_codes = rvq_codes
     ops.rvq_expand = rvq_expand
+    ops.rvq_fused = rvq_fused
+    ops.rvq_cross_prep = lambda wi, wo, bo: (torch.zeros(wi.shape[0], wi.shape[0], 8, 8),
+                                             torch.zeros(wi.shape[0], 8))
     ops.masked_loss = lambda l, m: torch.zeros(())
 
 
@@ -74,7 +93,8 @@ def main():
     with torch.no_grad():
         m(torch.zeros(args.batch, 1, 44100), 44100, None, 1.0)
     rows = list(csv.DictReader(open(args.trace)))
-    conv = [r for r in rows if "conv_mfma_kernel" in r["Kernel_Name"] or "conv_small" in r["Kernel_Name"]]
+    conv = [r for r in rows if any(k in r["Kernel_Name"] for k in
+                                   ("conv_mfma_kernel", "conv_small", "ru_fused_kernel"))]
     step = conv[-len(CALLS):]
     tot_t = tot_f = 0.0
     print(f"{'layer':42s} {'kernel':22s} {'us':>9s} {'GFLOP':>8s} {'TF/s':>7s} {'%pk':>5s}")
@@ -82,11 +102,13 @@ def main():
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         kn = r["Kernel_Name"]
         i = kn.find("<")
-        kn = ("mfma" + kn[i:kn.find(">") + 1]) if "mfma" in kn else "small" + kn[kn.find("<"):kn.find(">") + 1]
+        pre = "mfma" if "mfma" in kn else ("ru" if "ru_fused" in kn else "small")
+        kn = pre + kn[i:kn.find(">") + 1]
         tf = c[8] / (us * 1e-6) / 1e12
         tot_t += us
         tot_f += c[8]
-        desc = f"{c[0]} {c[1]}->{c[2]} k{c[3]} s{c[4]} d{c[5]} T{c[6]}{' +res' if c[9] else ''}"
+        desc = (f"RU {c[1]} k7+k1 d{c[5]} T{c[6]} (fused)" if c[0] == "RU" else
+                f"{c[0]} {c[1]}->{c[2]} k{c[3]} s{c[4]} d{c[5]} T{c[6]}{' +res' if c[9] else ''}")
         print(f"{desc:42s} {kn:22s} {us:9.1f} {c[8]/1e9:8.1f} {tf:7.1f} {tf/157.3*100:5.1f}")
     print(f"total conv: {tot_t/1e3:.2f} ms, {tot_f/1e12:.3f} TFLOP, {tot_f/(tot_t*1e-6)/1e12:.1f} TF/s")
 

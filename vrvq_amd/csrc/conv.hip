@@ -191,7 +191,8 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     if constexpr (kWide) if (wide) return launch_cfg<96, 256, 1, 8, KS>(a, batch, st);
     return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
   }
-  if (KS >= 3 && a.M % 128 != 0 && a.M % 192 == 0) {
+  if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
+    // (KS == 2 with up > 0: the polyphase ConvTranspose1d 192->96 s2, M = 192 phase rows)
     if constexpr (kWide) if (wide) return launch_cfg<192, 256, 2, 8, KS>(a, batch, st);
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }

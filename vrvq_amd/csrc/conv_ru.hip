@@ -8,10 +8,12 @@
 //                                                 prefetched a group of steps ahead, no barriers
 //   out      y = acc + b1 + x (y optional) and snake_next(y)   the conv.hip epilogue
 // Versus the two-launch form this removes the write + re-read of snake2(h) (2 C*T*4 bytes per
-// unit and clip) and the separate k=1 launch. The MFMA K order of both phases and every
-// epilogue expression are those of the two launches, so the output is bit-identical to them.
-// Instantiated for C in {64, 96, 128, 192} (the long-time-axis blocks); other widths use the
-// two-launch form.
+// unit and clip) and the separate k=1 launch. Every epilogue expression and the phase-2 K order
+// are those of the two launches; the phase-1 K order too wherever the two-launch k7 uses the
+// same tile height (C <= 192), so there the output is bit-identical to them.
+// Instantiated for C in {64, 96, 128, 192, 256} (the long-time-axis blocks). Measured and
+// dropped: C = 384 (an 8-wave 384x64 tile ran 8 % slower than the two launches); the 512 /
+// 768-channel units (T = 696) use the two-launch form.
 #include "common.h"
 #include "conv_core.h"
 
@@ -178,6 +180,7 @@ extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch,
     case 96: return launch_ru<96, 128, 1, 4>(ra, batch, st);
     case 128: return launch_ru<128, 128, 2, 4>(ra, batch, st);
     case 192: return launch_ru<192, 64, 2, 4>(ra, batch, st);
+    case 256: return launch_ru<256, 64, 2, 4>(ra, batch, st);
     default: return VRVQ_ERR_UNSUPPORTED;
   }
 }

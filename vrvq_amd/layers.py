@@ -171,8 +171,8 @@ class ResidualUnit(nn.Module):
         """Chained form: x_snk = block[0](x) was produced by the previous layer's epilogue.
         For C in ops.RU_FUSED_CHANNELS one launch (vrvq_residual_unit: block[2](h) stays in
         LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
-        k1 conv adds the skip. Either way the output is (y if want_raw, out_snake(y)), bit for
-        bit the same."""
+        k1 conv adds the skip. Either way the output is (y if want_raw, out_snake(y)) (bit for
+        bit the same for C <= 192, include/vrvq.h)."""
         if self.fused and x.shape[1] in ops.RU_FUSED_CHANNELS:
             w7, cp7 = self.block[1].prepared()
             w1, cp1 = self.block[3].prepared()

@@ -160,7 +160,7 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
     return y if out_snake is None else (y, ys)
 
 
-RU_FUSED_CHANNELS = (64, 96, 128, 192)
+RU_FUSED_CHANNELS = (64, 96, 128, 192, 256)
 
 
 def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad: int,
