@@ -46,6 +46,20 @@ def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024)
     return B * T * per_frame + weights
 
 
+def rvq_pmc_traffic(kernel: str = "rvq_fused_kernel<4>"):
+    """HBM bytes per launch of the RVQ kernel from the newest committed PMC measurement
+    (profiles/*_rvq_pmc.json: rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, made by
+    tools/gpu/pmc_rvq.sh at this workload). bench.py cannot collect PMC counters itself (they
+    need their own rocprofv3 passes), so it reports that measurement and names its file."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_rvq_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    return (int(k["total"]) if k else None), os.path.relpath(files[-1], REPO)
+
+
 def conv_flops(model, B: int, L: int) -> float:
     """Algorithmic conv FLOPs of one encode+decode (2 * MACs over every conv layer), counted
     from the layer geometry: the implicit GEMM's M x N x K per layer."""
@@ -233,6 +247,8 @@ def main():
     conv_ms = ms_per_step - rvq_ms
     conv_tflops = flops / (conv_ms * 1e-3) / 1e12
 
+    traffic, traffic_src = rvq_pmc_traffic() if (args.batch, args.n_codebooks) == (32, 8) \
+        else (None, None)
     if rank == 0:
         res = {
             "metric": "audio-sec/s encode+RVQ+decode, 44.1 kHz batch-32, 1->8 MI355X; RVQ HBM GB/s",
@@ -254,7 +270,7 @@ def main():
                        "parallelism": f"dp{world} (replicas, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "rvq_fused_kernel (residual chain + z_q_is stream + gating)",
                          "bytes_per_launch": byt, "path_us": round(rvq_ms * 1e3, 2),
                          "launch_us": {k: round(v * 1e3, 2) for k, v in per.items()}},
