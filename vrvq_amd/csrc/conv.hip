@@ -162,6 +162,14 @@ static int conv_variant() {  // tuning override: VRVQ_CONV_VARIANT=0 (4-wave) | 
   return v;
 }
 
+static int conv_bn_rule() {  // tuning override: VRVQ_CONV_BN_RULE=0 (minimise padding) | 1
+  static const int v = [] {  // (128 wide unless it pads more than 15 % of the columns)
+    const char* e = getenv("VRVQ_CONV_BN_RULE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -174,7 +182,8 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     const long long blocks96 = (long long)((a.M + 127) / 128) * batch;
     bn = blocks96 >= 384 ? 96 : 32;
   }
-  else if (a.ng < 4096 && waste(64) * 10 < waste(128) * 7) bn = 64;
+  else if (a.ng < 4096 && conv_bn_rule() == 0 && waste(64) * 10 < waste(128) * 7) bn = 64;
+  else if (a.ng < 4096 && conv_bn_rule() == 1 && waste(128) * 100 > a.ng * 15) bn = 64;
   else bn = 128;
   if (a.M <= 32) return launch_cfg<32, 128, 1, 4, KS>(a, batch, st);
   if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
