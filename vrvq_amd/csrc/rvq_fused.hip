@@ -122,8 +122,7 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
   // LDS: one array per role, so the compiler's LDS-DMA wait tracking can tell the DMA targets
   // (cbn, c2, raw, W_out) from the arrays read while a DMA is in flight (tile, red, wv, ...).
   __shared__ __attribute__((aligned(16))) float cbn_s[N * FU_CD];
-  __shared__ __attribute__((aligned(16))) float c2_s[N];
-  __shared__ __attribute__((aligned(16))) float raw_s[N * FU_CD];
+  __shared__ __attribute__((aligned(16))) float cand_s[FU_FG * 4 * FU_FPG * FU_CD];  // raw rows
   __shared__ __attribute__((aligned(16))) float wo_s[FU_D * FU_CD];
   __shared__ __attribute__((aligned(16))) float bo_s[FU_D];
   __shared__ __attribute__((aligned(16))) float tile[FU_D * FU_TS];
@@ -131,7 +130,8 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) float dbs[FU_FG * 32];
   __shared__ __attribute__((aligned(16))) int ibs[FU_FG * 32];
   __shared__ __attribute__((aligned(16))) float wv_all[FU_NW * FU_WV];
-  static_assert((N * FU_CD * 2 + N + FU_D * FU_CD + FU_D + FU_D * FU_TS + FU_FG * 4 * 48 + FU_FG * 64 +
+  __shared__ __attribute__((aligned(16))) float warm_s[256];  // L2 warm-up DMA sink (never read)
+  static_assert((256 + N * FU_CD + FU_FG * 4 * FU_FPG * FU_CD + FU_D * FU_CD + FU_D + FU_D * FU_TS + FU_FG * 4 * 48 + FU_FG * 64 +
                  FU_NW * FU_WV) * 4 <= 160 * 1024, "LDS budget");
 
   // ---- unit: XCD-major mapping (workgroup w runs on XCD w % 8) ----
@@ -163,19 +163,18 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
                                          : INFINITY;  // this lane's frame (mask output)
 
   // ---- stage weights ----
-  // Codebooks and W_out go HBM/L2 -> LDS by LDS-DMA (no registers in flight):
-  //   cbn / c2 (i+1)   issued after barrier B(i)   (the stage-i distance scans are done),
+  // The normalised codebook and W_out / b_out go HBM/L2 -> LDS by LDS-DMA (no registers):
+  //   cbn (i+1)        issued after barrier B(i) (the stage-i distance scans are done),
   //                    landed at the vmcnt(0) before barrier A(i+1);
-  //   raw cb, W_out / b_out(i) issued after barrier A(i)   (the stage-(i-1) gathers / out_proj are
-  //                    done), landed at the vmcnt before barrier B(i) — issued ahead of the
-  //                    z_q_is stores, so "all but the last FU_TR VMEM ops" covers them.
-  // W_in (i+1) / b_in go to registers after barrier B(i). b_out travels with W_out.
+  //   W_out / b_out(i) issued after barrier A(i) (the stage-(i-1) out_proj reads are done),
+  //                    landed at the vmcnt(0) before barrier B(i).
+  // Not streamed: |c|^2 is recomputed from the cbn row (codebook_prep's expression), and of the
+  // raw codebook only the rows of each wave's argmin candidates are gathered from L2 (below).
+  // W_in (i+1) / b_in go to registers after barrier B(i).
   auto dma_cbn = [&](int i) {
     dma_chunks(a.cbn + (size_t)i * N * FU_CD, cbn_s, N * FU_CD / 256, wave, lane);
-    dma_chunks(a.c2 + (size_t)i * N, c2_s, N / 256, wave, lane);
   };
-  auto dma_raw_wo = [&](int i) {
-    dma_chunks(a.cb + (size_t)i * N * FU_CD, raw_s, N * FU_CD / 256, wave, lane);
+  auto dma_wo = [&](int i) {
     dma_chunks(a.w_out + (size_t)i * FU_D * FU_CD, wo_s, FU_D * FU_CD / 256, wave, lane);
     dma_chunks(a.b_out + (size_t)i * FU_D, bo_s, FU_D / 256, wave, lane);
   };
@@ -189,9 +188,10 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     }
   };
   // [D][T] row block (columns t0 .. t0+nf) from the LDS tile: 16-lane segments, one row each,
-  // 48 rows per pass. Per-lane offsets are loop-invariant single VGPRs; each pass advances the
-  // wave-uniform row pointer (SGPRs) and the LDS immediate offset. Waves issue FU_TR - 1 or
-  // FU_TR store instructions.
+  // 32 rows per pass. Per-lane offsets are loop-invariant single VGPRs; each pass advances the
+  // wave-uniform row pointer (SGPRs) and the LDS immediate offset. (Measured: 3 lanes x dwordx4
+  // per row issues 5x fewer store instructions but ran 40 % slower — the rows are only
+  // dword-aligned, T being odd.)
   const int ss = lane & 15, sub = lane >> 4;
   const unsigned g_off = (unsigned)((wave * 4 + sub) * T + t0 + ss);
   const float* t_lane = tile + (wave * 4 + sub) * FU_TS + ss;
@@ -208,6 +208,27 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
   dma_cbn(0);
   load_wi(0);
   float bin_nx = a.b_in[kl];
+  // L2 warm-up: the workgroups of one XCD (workgroup w runs on XCD w % 8) together touch every
+  // stage's weights once (W_in, cbn, W_out, b_out: ~100 KB per stage), each 1/per_xcd of them,
+  // as LDS-DMA pieces into a sink that is never read. Every later per-stage DMA / W_in load then
+  // hits this XCD's L2 instead of taking a fabric / HBM miss on the chain's critical path. Lands
+  // at the vmcnt(0) before barrier A of stage 0.
+  {
+    const int xj = bid >> 3;
+    auto warm = [&](const float* base, int nchunks) {
+      for (int q = xj * FU_NW + wave; q < nchunks; q += a.per_xcd * FU_NW) {
+        const float* gp = base + q * 256 + lane * 4;
+        const unsigned lds =
+            (unsigned)(size_t)(__attribute__((address_space(3))) float*)(warm_s);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                     :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(gp) : "memory", "m0");
+      }
+    };
+    warm(a.w_in_t, nq * FU_D * FU_CD / 256);
+    warm(a.cbn, nq * N * FU_CD / 256);
+    warm(a.w_out, nq * FU_D * FU_CD / 256);
+    warm(a.b_out, nq * FU_D / 256);
+  }
 
   // ---- residual tile z[b, :, t0 .. t0+nf) -> LDS -> registers ----
   {
@@ -278,7 +299,7 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" :: "v"(bin) : "memory");
     lds_barrier();  // ------------------------------------------------------------------ A
     FSTAMP(2);
-    dma_raw_wo(i);
+    dma_wo(i);
     // z_q_is of the previous stage: tile -> HBM
     const bool tile_out = i > 0 && a.z_q_is;
     if (tile_out) store_tile(a.z_q_is + ((size_t)b * nq + (i - 1)) * FU_D * T);
@@ -326,7 +347,9 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
         const float4 c0 = *reinterpret_cast<const float4*>(cbn_s + n * FU_CD);
         const float4 c1 = *reinterpret_cast<const float4*>(cbn_s + n * FU_CD + 4);
         const float ck[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        const float cc = c2_s[n];
+        float cc = 0.0f;  // |c|^2 of the normalised row, codebook_prep's fmaf chain
+#pragma unroll
+        for (int k = 0; k < FU_CD; ++k) cc = fmaf(ck[k], ck[k], cc);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           // dot in k order (mul, then fma chain), then (sum e^2 - 2 e.c) + sum c^2
@@ -348,12 +371,15 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
       dbs[(g * 4 + wg) * 8 + fl] = best[0];
       ibs[(g * 4 + wg) * 8 + fl] = bidx[0];
     }
+    // raw codebook row of this wave's candidate (the final winner is one of the 4 waves'
+    // candidates): an L2 gather of 32 B per frame instead of streaming the 32 KB raw codebook
+    if (lrole) {
+      const int cix = (bidx[0] >= 0 && bidx[0] < N) ? bidx[0] : 0;
+      cand_s[((g * 4 + wg) * FU_FPG + fl) * FU_CD + kl] = a.cb[((size_t)i * N + cix) * FU_CD + kl];
+    }
     FSTAMP(4);
-    // raw codebook / W_out DMA of this stage landed: only the z_q_is stores (>= FU_TR - 1 per
-    // wave) and the latents store were issued after it
-    static_assert(FU_TR - 1 >= 30, "vmcnt below");
-    if (tile_out) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // W_out / b_out DMA of this stage and the candidate rows landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();  // ------------------------------------------------------------------ B
     FSTAMP(5);
     if (more) {
@@ -364,15 +390,21 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     // (5) final argmin, raw codeword, loss, codes, mask, straight-through vector
     {
       float bd = INFINITY;
-      int bi = 0;
+      int bi = 0, wsel = 0;
       if (lrole) {
         bd = dbs[(g * 4) * 8 + fl];
         bi = ibs[(g * 4) * 8 + fl];
 #pragma unroll
-        for (int w = 1; w < 4; ++w)
-          vrvq::amin(bd, bi, dbs[(g * 4 + w) * 8 + fl], ibs[(g * 4 + w) * 8 + fl]);
+        for (int w = 1; w < 4; ++w) {
+          const float od = dbs[(g * 4 + w) * 8 + fl];
+          const int oi = ibs[(g * 4 + w) * 8 + fl];
+          const bool take = (od < bd) | ((od == bd) & (oi < bi));  // vrvq::amin, + the wave
+          bd = take ? od : bd;
+          bi = take ? oi : bi;
+          wsel = take ? w : wsel;
+        }
       }
-      const float zq = raw_s[bi * FU_CD + kl];
+      const float zq = lrole ? cand_s[((g * 4 + wsel) * FU_FPG + fl) * FU_CD + kl] : 0.0f;
       const float st = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
       const float diff = ze - zq;
       const float l2 = vrvq::sum8(diff * diff, lane);
