@@ -340,7 +340,7 @@ def _rvq_fp64_reference(z, st, imp, level):
     return codes, z_q_is, z_q, mask
 
 
-@pytest.mark.parametrize("path", ["encode", "fused"])
+@pytest.mark.parametrize("path", ["encode", "fused", "split"])
 @pytest.mark.parametrize("nq,ncode,B,T,vbr", [
     (8, 1024, 3, 87, True), (8, 1024, 2, 1, True), (8, 1024, 2, 13, True), (8, 1024, 1, 25, False),
     (1, 1024, 4, 87, False), (32, 1024, 2, 87, True), (4, 256, 3, 40, True), (4, 512, 2, 87, True),
@@ -364,6 +364,9 @@ def test_rvq_paths_vs_fp64_and_two_kernel(path, nq, ncode, B, T, vbr):
     level = 0.75
     if path == "encode":
         codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=level)
+    elif path == "split":
+        codes, lat, loss, zqis, zq, mask = ops.rvq_split(z, *st.codes_args(), imp=imp, level=level)
+        assert not ops.rvq_split_error(z.device)
     else:
         codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=level)
     c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())
@@ -383,7 +386,7 @@ def test_rvq_paths_vs_fp64_and_two_kernel(path, nq, ncode, B, T, vbr):
     assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)
 
 
-@pytest.mark.parametrize("path", ["encode", "fused"])
+@pytest.mark.parametrize("path", ["encode", "fused", "split"])
 def test_rvq_big_batch_properties(path):
     """BASELINE config 3 shape (B=64, 32 codebooks): two rounds of workgroups per CU."""
     gen = torch.Generator().manual_seed(5)
@@ -398,6 +401,9 @@ def test_rvq_big_batch_properties(path):
     imp = torch.rand(64, 87, generator=gen).to(DEV)
     if path == "encode":
         codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=1.0)
+    elif path == "split":
+        codes, lat, loss, zqis, zq, mask = ops.rvq_split(z, *st.codes_args(), imp=imp, level=1.0)
+        assert not ops.rvq_split_error(z.device)
     else:
         codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=1.0)
     c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--nq", type=int, default=8)
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--only", choices=["encode", "fused", "pair", "all"], default="all")
+    ap.add_argument("--only", choices=["encode", "fused", "pair", "split", "all"], default="all")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -30,8 +30,8 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(1)
     z = (torch.randn(args.batch, 1024, args.frames, generator=g) * 0.3).to(dev)
     imp = torch.rand(args.batch, args.frames, generator=g).to(dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
-    tf, tc, te, tp, tch, tx = [], [], [], [], [], []
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
+    tf, tc, te, tp, tch, tx, ts = [], [], [], [], [], [], []
     for it in range(args.iters):
         ev[4].record()
         if args.only in ("encode", "all"):
@@ -55,6 +55,10 @@ def main():
         if args.only in ("pair", "all"):
             ops.rvq_expand(zst, st.w_out, st.b_out, imp, 1.0)
         ev[3].record()
+        ev[8].record()
+        if args.only in ("split", "all"):
+            ops.rvq_split(z, *st.codes_args(), imp=imp, level=1.0)
+        ev[9].record()
         torch.cuda.synchronize()
         if it >= 5:
             tf.append(ev[0].elapsed_time(ev[1]) * 1e3)
@@ -63,6 +67,7 @@ def main():
             tp.append(ev[4].elapsed_time(ev[5]) * 1e3)
             tch.append(ev[5].elapsed_time(ev[6]) * 1e3)
             tx.append(ev[6].elapsed_time(ev[7]) * 1e3)
+            ts.append(ev[8].elapsed_time(ev[9]) * 1e3)
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     byt = args.batch * args.frames * (1024 * 4 * (2 + args.nq) + 4 + args.nq * (8 + 32 + 8))
     enc = med(tp) + med(tch) + med(tx)
@@ -72,6 +77,17 @@ def main():
     print(f"B={args.batch} nq={args.nq} T={args.frames}: fused median {med(tf):.1f} us "
           f"({byt / med(tf) / 1e3:.0f} GB/s algorithmic); codes {med(tc):.1f} us, "
           f"expand {med(te):.1f} us")
+    if args.only in ("split", "all"):
+        print(f"B={args.batch} nq={args.nq} T={args.frames}: split median {med(ts):.1f} us "
+              f"({byt / med(ts) / 1e3:.0f} GB/s algorithmic)")
+        if args.only == "all":
+            a = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=1.0)
+            b = ops.rvq_split(z, *st.codes_args(), imp=imp, level=1.0)
+            torch.cuda.synchronize()
+            agree = (a[0] == b[0]).float().mean().item()
+            dz = (a[3] - b[3]).abs().max().item()
+            print(f"  split vs fused: codes agree {agree:.6f}, z_q_is max |diff| {dz:.3e}, "
+                  f"error flag {ops.rvq_split_error(dev)}")
 
 if __name__ == "__main__":
     main()

@@ -305,6 +305,57 @@ def rvq_fused(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp=None, level: float
     return codes, latents, loss_pf, z_q_is, z_q, mask
 
 
+_split_ws = {}  # device index -> zero-filled workspace of vrvq_rvq_split (left zero by every launch)
+
+
+def _split_workspace(dev: torch.device, B: int, T: int) -> torch.Tensor:
+    n = ctypes.c_longlong(0)
+    _lib.call("vrvq_rvq_split_workspace", B, T, ctypes.byref(n))
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ws = _split_ws.get(key)
+    if ws is None or ws.numel() < n.value:
+        ws = torch.zeros(max(n.value, 1 << 20), device=dev, dtype=torch.uint8)
+        _split_ws[key] = ws
+    return ws
+
+
+def rvq_split_error(dev: torch.device) -> bool:
+    """True if a vrvq_rvq_split launch on `dev` timed out in a group exchange (its outputs are
+    invalid); re-zeroes the workspace. Synchronises the device."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ws = _split_ws.get(key)
+    if ws is None:
+        return False
+    bad = bool(ws[:4].any().item())
+    if bad:
+        ws.zero_()
+    return bad
+
+
+def rvq_split(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp=None, level: float = 1.0,
+              want_z_q_is: bool = True, want_mask: bool = True):
+    """Channel-split single launch (vrvq_rvq_split): the outputs of rvq_fused, computed by
+    groups of 8 workgroups exchanging 8-dim partials / argmin candidates through L2."""
+    _chk(z, "z"); dev = z.device
+    for t, n in ((w_in_t, "w_in_t"), (b_in, "b_in"), (cb, "cb"), (cbn, "cbn"), (c2, "c2"),
+                 (w_out, "w_out"), (b_out, "b_out")):
+        _chk(t, n, device=dev)
+    _chk(imp, "imp", device=dev)
+    B, D, T = z.shape
+    nq, N, d = cb.shape
+    codes = torch.empty((B, nq, T), device=dev, dtype=torch.int64)
+    latents = torch.empty((B, nq * d, T), device=dev, dtype=torch.float32)
+    loss_pf = torch.empty((B, nq, T), device=dev, dtype=torch.float32)
+    z_q_is = torch.empty((B, nq, D, T), device=dev, dtype=torch.float32) if want_z_q_is else None
+    z_q = torch.empty((B, D, T), device=dev, dtype=torch.float32)
+    mask = torch.empty((B, nq, T), device=dev, dtype=torch.float32) if want_mask else None
+    ws = _split_workspace(dev, B, T)
+    _lib.call("vrvq_rvq_split", _p(z), B, D, T, nq, N, d, _p(w_in_t), _p(b_in), _p(cb), _p(cbn),
+              _p(c2), _p(w_out), _p(b_out), _p(imp), float(level), _p(codes), _p(latents),
+              _p(loss_pf), _p(z_q_is), _p(z_q), _p(mask), _p(ws), ws.numel(), _stream(z))
+    return codes, latents, loss_pf, z_q_is, z_q, mask
+
+
 def masked_loss(loss_pf: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
     _chk(loss_pf, "loss_pf"); _chk(mask, "mask", device=loss_pf.device)
     B, nq, T = loss_pf.shape
