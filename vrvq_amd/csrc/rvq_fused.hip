@@ -213,6 +213,8 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
   // as LDS-DMA pieces into a sink that is never read. Every later per-stage DMA / W_in load then
   // hits this XCD's L2 instead of taking a fabric / HBM miss on the chain's critical path. Lands
   // at the vmcnt(0) before barrier A of stage 0.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else here uses it
   {
     const int xj = bid >> 3;
     auto warm = [&](const float* base, int nchunks) {
@@ -229,6 +231,7 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     warm(a.w_out, nq * FU_D * FU_CD / 256);
     warm(a.b_out, nq * FU_D / 256);
   }
+#pragma clang diagnostic pop
 
   // ---- residual tile z[b, :, t0 .. t0+nf) -> LDS -> registers ----
   {
