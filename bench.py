@@ -196,6 +196,7 @@ def main():
 
     import vrvq_amd
     from vrvq_amd.recipe import load_recipe, synthetic_audio
+    from vrvq_amd.replicas import shard_seed, throughput, timed_steps
 
     kwargs = dict(encoder_dim=64, encoder_rates=[2, 4, 8, 8], decoder_dim=1536,
                   decoder_rates=[8, 8, 4, 2], n_codebooks=args.n_codebooks, codebook_size=1024,
@@ -203,7 +204,8 @@ def main():
     model = vrvq_amd.DAC_VRVQ(**kwargs)
     load_recipe(model, seed=0)
     model = model.to(dev).eval()
-    audio = torch.from_numpy(synthetic_audio(args.batch, CLIP_SAMPLES, seed=1234 + rank)).to(dev)
+    audio = synthetic_audio(args.batch, CLIP_SAMPLES, seed=shard_seed(1234, rank))
+    audio = torch.from_numpy(audio).to(dev)
 
     timer = RvqTimer()
     install_rvq_timer(timer)
@@ -212,29 +214,18 @@ def main():
         with torch.no_grad():
             return model(audio, SR, None, args.level)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timer.enabled = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    timer.enabled = False
-    dt = t1 - t0
-    if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    def timer_on():
+        timer.enabled = True
+
+    def timer_off():
+        timer.enabled = False
+
+    res_t = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize, device=dev,
+                        on_start=timer_on, on_stop=timer_off)
+    out = res_t.last
+    dt = res_t.seconds
     ms_per_step = dt / args.steps * 1e3
-    total_clips = args.batch * world * args.steps
-    value = total_clips * (CLIP_SAMPLES / SR) / dt
+    value = throughput(args.batch * CLIP_SAMPLES / SR, res_t)
 
     durs = timer.durations_ms()
     T = out["codes"].shape[-1]
