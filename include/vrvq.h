@@ -236,6 +236,15 @@ int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames, int nq, in
                     const float* w_out, const float* b_out, const float* imp, float level,
                     float* z_q_is, float* z_q, float* mask, vrvq_stream_t stream);
 
+/* Codes -> latents gather (decode_code of every stage, models/quantize.py:81-85, as used by
+ * ResidualVectorQuantize.from_codes, :217-249):
+ *   z_p[b, i*d + k, t] = cb[i][codes[b,i,t]][k]   (raw codebook rows, [B][nq*d][T]) or NULL
+ *   zst[b][i][t][k]    = the same rows, the input layout of vrvq_rvq_expand, or NULL
+ * A code outside [0, ncode) sets *err = 1 (err may be NULL) and reads row 0: the caller raises
+ * IndexError as F.embedding does. */
+int vrvq_rvq_gather(const int64_t* codes, int batch, int nq, int frames, const float* cb,
+                    int ncode, int cdim, float* zst, float* z_p, int* err, vrvq_stream_t stream);
+
 /* Masked loss reduction (models/quantize.py:422-423): out[0] = (loss_pf*mask).sum(1).mean().
  * One workgroup, fixed order (deterministic). */
 int vrvq_masked_loss(const float* loss_pf, const float* mask, int batch, int nq, int frames,

@@ -184,6 +184,27 @@ class Oracle:
         z_q_i = self.conv(z_st, p + ".out_proj")
         return z_q_i, loss, idx.astype(np.int64), z_e
 
+    # models/quantize.py:217-249 (ResidualVectorQuantize.from_codes): decode_code (:81-85,
+    # raw codebook rows) -> out_proj per stage, z_q = sum in stage order; with `mask` the
+    # masked sum of scripts/inference.py:99-100 (VBR).
+    def from_codes(self, codes, mask=None):
+        B, n, T = codes.shape
+        z_p, z_q_is = [], []
+        for i in range(n):
+            p = f"quantizer.quantizers.{i}"
+            cb = self.sd[p + ".codebook.weight"]
+            zp = cb[codes[:, i]].transpose(0, 2, 1).astype(F32)         # (B, d, T)
+            z_p.append(zp)
+            z_q_is.append(self.conv(zp, p + ".out_proj"))
+        z_q_is = np.stack(z_q_is, axis=1)
+        if mask is None:
+            z_q = np.zeros(z_q_is[:, 0].shape, F32)
+            for i in range(n):
+                z_q = z_q + z_q_is[:, i]
+        else:
+            z_q = masked_sum(z_q_is, mask)
+        return z_q, np.concatenate(z_p, axis=1), z_q_is
+
     # models/quantize.py:328-443 (eval) and :136-214 (CBR eval)
     def quantize(self, z, n_quantizers=None, feat=None, level=1.0):
         nq = self.n_codebooks

@@ -192,6 +192,39 @@ def rvq_stress_fixture(DAC, kw, name, manifest, batch=4, frames=50, seed=7):
     print(name, "gap", min(gaps))
 
 
+def from_codes_fixture(DAC, kw, name, manifest, batch=2, frames=40, seed=5, vbr=False):
+    """codes -> z_q / z_p / z_q_is / audio. CBR: the reference's own
+    ResidualVectorQuantize.from_codes (models/quantize.py:217-249). VBR (whose from_codes raises
+    NotImplementedError in the reference): the same per-stage decode_code + out_proj of the
+    reference's quantizers and the masked sum of scripts/inference.py:99-100."""
+    model = build(DAC, kw)
+    q = model.quantizer
+    nq, N = len(q.quantizers), q.quantizers[0].codebook_size
+    g = torch.Generator().manual_seed(seed)
+    codes = torch.randint(0, N, (batch, nq, frames), generator=g, dtype=torch.int64)
+    codes[0, :, 0] = 0
+    codes[-1, :, -1] = N - 1
+    res = {"codes": codes.numpy()}
+    with torch.no_grad():
+        if not vbr:
+            z_q, z_p, _, z_q_is = q.from_codes(codes, return_z_q_is=True)
+        else:
+            z_p = torch.cat([qi.decode_code(codes[:, i]) for i, qi in enumerate(q.quantizers)], 1)
+            z_q_is = torch.stack([qi.out_proj(qi.decode_code(codes[:, i]))
+                                  for i, qi in enumerate(q.quantizers)], dim=1)
+            s = torch.rand(batch, 1, frames, generator=g) * nq
+            mask = torch.stack([(s[:, 0] - i >= 0).float() for i in range(nq)], dim=1)
+            z_q = torch.sum(z_q_is * mask[:, :, None, :], dim=1, keepdim=False)
+            res["mask"] = mask.numpy()
+        audio = model.decode(z_q)
+    res.update(z_q=z_q.numpy(), z_p=z_p.numpy(), z_q_is=z_q_is.numpy(), audio=audio.numpy())
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+    manifest[name] = {"kwargs": kw, "batch": batch, "frames": frames, "codes_seed": seed,
+                      "weight_seed": 0, "vbr": vbr,
+                      "state_dict": {k: list(v.shape) for k, v in model.state_dict().items()}}
+    print(name, "nq", nq, "audio", tuple(audio.shape))
+
+
 def mask_kat(ref_utils, manifest):
     s = torch.tensor(MASK_KAT_S, dtype=torch.float32).reshape(1, 1, -1)
     out = {}
@@ -203,12 +236,28 @@ def mask_kat(ref_utils, manifest):
     manifest["mask_kat"] = {"s": [float(v) for v in s.reshape(-1)], "results": out}
 
 
+def from_codes_all(DAC, ref, manifest):
+    from_codes_fixture(DAC, yml_kwargs(ref, "conf/original_dac/cbr.yml"), "golden_from_codes_cbr",
+                       manifest)
+    from_codes_fixture(DAC, yml_kwargs(ref, "conf/base.yml"), "golden_from_codes_vbr", manifest,
+                       seed=6, vbr=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.environ.get("VRVQ_REFERENCE", "/root/reference"))
+    ap.add_argument("--only", choices=["from_codes"], default=None,
+                    help="regenerate only these fixtures and merge them into manifest.json")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
     DAC, ref_utils = load_ref(args.ref)
+    if args.only == "from_codes":
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        from_codes_all(DAC, args.ref, manifest)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, default=float)
+        return
     manifest = {"generator": "tests/golden/make_golden.py", "torch": torch.__version__,
                 "reference": "lixinghe1999/VRVQ @ 2025-07-25 (/root/reference)",
                 "levels": LEVELS}
@@ -227,6 +276,7 @@ def main():
     rvq_stress_fixture(DAC, base, "golden_rvq_stress_nq8", manifest)
     rvq_stress_fixture(DAC, k32, "golden_rvq_stress_nq32", manifest, batch=2, frames=40, seed=11)
     mask_kat(ref_utils, manifest)
+    from_codes_all(DAC, args.ref, manifest)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, default=float)
 

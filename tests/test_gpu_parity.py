@@ -464,3 +464,68 @@ def test_residual_unit_fused_vs_two_launch(C, T, dil, want_raw):
         ref = x.double() + F.conv1d(hs, w1, ru.block[3].bias.double())
         ys_ref = _snake_ref(ref, nxt.alpha.reshape(-1).double())
     assert rel_err(ys_f.cpu().numpy(), ys_ref.cpu().numpy()) < 1e-5
+
+
+# ------------------------------------------------------------------ codes -> latents -> audio
+@pytest.mark.parametrize("name", ["golden_from_codes_cbr", "golden_from_codes_vbr"])
+def test_from_codes_vs_reference(manifest, name):
+    """ResidualVectorQuantize.from_codes (models/quantize.py:217-249) through vrvq_rvq_gather +
+    vrvq_rvq_expand, then decode; VBR with the mask (scripts/inference.py:99-100 masked sum)."""
+    m = manifest[name]
+    g = load_golden(name)
+    model = model_for(manifest, name)
+    codes = t(g["codes"])
+    with torch.no_grad():
+        if m["vbr"]:
+            z_q, z_p, codes_out, z_q_is = model.quantizer.from_codes(
+                codes, return_z_q_is=True, mask_imp=t(g["mask"]))
+        else:
+            z_q, z_p, codes_out, z_q_is = model.quantizer.from_codes(codes, return_z_q_is=True)
+        audio = model.decode(z_q)
+    np.testing.assert_array_equal(z_p.cpu().numpy(), g["z_p"])   # bit-exact gather
+    np.testing.assert_array_equal(codes_out.cpu().numpy(), g["codes"])
+    assert rel_err(z_q_is.cpu().numpy(), g["z_q_is"]) < TOL
+    assert rel_err(z_q.cpu().numpy(), g["z_q"]) < TOL
+    assert rel_err(audio.cpu().numpy(), g["audio"]) < TOL
+    # without z_q_is: same z_q, and the plain (unmasked) sum for CBR
+    with torch.no_grad():
+        out = model.quantizer.from_codes(codes) if not m["vbr"] else \
+            model.quantizer.from_codes(codes, mask_imp=t(g["mask"]))
+    assert len(out) == 3
+    assert torch.equal(out[0], z_q)
+
+
+def test_from_codes_prefix_and_errors(manifest):
+    model = model_for(manifest, "golden_from_codes_cbr")
+    g = load_golden("golden_from_codes_cbr")
+    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0),
+               **manifest["golden_from_codes_cbr"]["kwargs"])
+    codes = g["codes"][:, :3].copy()                     # fewer codebooks than the model
+    z_q, z_p, _ = model.quantizer.from_codes(t(codes))
+    zq_o, zp_o, _ = o.from_codes(codes)
+    np.testing.assert_array_equal(z_p.cpu().numpy(), zp_o)
+    assert rel_err(z_q.cpu().numpy(), zq_o) < TOL
+    bad = codes.copy()
+    bad[0, 1, 5] = 1024                                  # == codebook_size
+    with pytest.raises(IndexError):
+        model.quantizer.from_codes(t(bad))
+    bad[0, 1, 5] = -1
+    with pytest.raises(IndexError):
+        model.quantizer.from_codes(t(bad))
+    too_many = np.zeros((1, model.quantizer.n_codebooks + 1, 4), np.int64)
+    with pytest.raises(IndexError):
+        model.quantizer.from_codes(t(too_many))
+
+
+def test_encode_from_codes_roundtrip_full_batch(manifest):
+    """Size-independent property at BASELINE batch 32: encode -> codes -> from_codes with the
+    encode's mask reproduces the encode's z_q (z_q_i from raw rows vs the straight-through
+    z_e + (z_q - z_e): equal up to fp32 rounding) and its z_q_is."""
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(32, 44100, seed=99))
+    with torch.no_grad():
+        enc = model.encode(model.preprocess(audio, 44100), None, 1.0)
+        z_q, z_p, _, z_q_is = model.quantizer.from_codes(enc["codes"], return_z_q_is=True,
+                                                         mask_imp=enc["mask_imp"])
+    assert rel_err(z_q.cpu().numpy(), enc["z_q"].cpu().numpy()) < TOL
+    assert rel_err(z_q_is.cpu().numpy(), enc["z_q_is"].cpu().numpy()) < TOL

@@ -139,6 +139,38 @@ unsigned grid_for(size_t total, unsigned block) {
   return (unsigned)g;
 }
 
+// decode_code of models/quantize.py:81-85 for every stage at once (the gather half of
+// ResidualVectorQuantize.from_codes, :217-249): z_p[b, i*d + k, t] = cb[i][codes[b,i,t]][k]
+// (raw, un-normalised rows) in the reference's latents layout, plus the same rows as
+// zst[b][i][t][d], the input layout of vrvq_rvq_expand (out_proj + masked sum). One thread per
+// (b, i, t); consecutive t -> consecutive lanes, so the z_p row stores coalesce.
+__global__ __launch_bounds__(256) void rvq_gather_kernel(const int64_t* __restrict__ codes,
+                                                         const float* __restrict__ cb, int batch,
+                                                         int nq, int frames, int ncode, int cdim,
+                                                         float* __restrict__ zst,
+                                                         float* __restrict__ z_p,
+                                                         int* __restrict__ err) {
+  const size_t n = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)batch * nq * frames;
+  if (n >= total) return;
+  const int t = (int)(n % frames);
+  const size_t bi = n / frames;            // b * nq + i
+  const int i = (int)(bi % nq);
+  long long c = codes[n];
+  if (c < 0 || c >= ncode) {               // F.embedding raises IndexError; report, read row 0
+    if (err) *err = 1;
+    c = 0;
+  }
+  const float* row = cb + ((size_t)i * ncode + (size_t)c) * cdim;
+  float* zs = zst ? zst + n * cdim : nullptr;
+  float* zp = z_p ? z_p + bi * cdim * frames + t : nullptr;
+  for (int k = 0; k < cdim; ++k) {
+    const float v = row[k];
+    if (zs) zs[k] = v;
+    if (zp) zp[(size_t)k * frames] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" const char* vrvq_status_string(int status) {
@@ -213,5 +245,16 @@ extern "C" int vrvq_bpf(const float* mask, const float* bits, int batch, int nq,
   VRVQ_CHECK_ARG(mask && bits && out && batch > 0 && nq > 0 && frames > 0);
   hipLaunchKernelGGL(bpf_kernel, dim3(1), dim3(1024), 0, as_stream(stream), mask, bits, batch, nq,
                      frames, out);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_rvq_gather(const int64_t* codes, int batch, int nq, int frames,
+                               const float* cb, int ncode, int cdim, float* zst, float* z_p,
+                               int* err, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(codes && cb && (zst || z_p) && batch > 0 && nq > 0 && frames > 0);
+  VRVQ_CHECK_ARG(ncode > 0 && cdim > 0);
+  const size_t total = (size_t)batch * nq * frames;
+  hipLaunchKernelGGL(rvq_gather_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     as_stream(stream), codes, cb, batch, nq, frames, ncode, cdim, zst, z_p, err);
   return vrvq_launch_status();
 }

@@ -65,6 +65,7 @@ struct FusedArgs {
   int nr;                // frame ranges per clip
   int units;             // B * nr
   int per_xcd;           // ceil(units / 8)
+  int nt_store;          // z_q_is rows stored non-temporal (keep the stage weights L2-resident)
   unsigned long long* stamps;  // diagnostic build only (-DVRVQ_STAMPS): [grid][nq][8]
 };
 
@@ -195,12 +196,15 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
   const int ss = lane & 15, sub = lane >> 4;
   const unsigned g_off = (unsigned)((wave * 4 + sub) * T + t0 + ss);
   const float* t_lane = tile + (wave * 4 + sub) * FU_TS + ss;
-  auto store_tile = [&](float* dst_base) {
+  auto store_tile = [&](float* dst_base, bool nt) {
     if (ss < nf) {
 #pragma unroll
       for (int k = 0; k < FU_TR; ++k) {
         if (k == FU_TR - 1 && (wave * 4 + 4 * FU_NW * k) >= FU_D) break;  // wave-uniform
-        *at(dst_base + (size_t)(4 * FU_NW * k) * T, g_off) = t_lane[4 * FU_NW * k * FU_TS];
+        float* p = at(dst_base + (size_t)(4 * FU_NW * k) * T, g_off);
+        const float v = t_lane[4 * FU_NW * k * FU_TS];
+        if (nt) __builtin_nontemporal_store(v, p);
+        else *p = v;
       }
     }
   };
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     dma_wo(i);
     // z_q_is of the previous stage: tile -> HBM
     const bool tile_out = i > 0 && a.z_q_is;
-    if (tile_out) store_tile(a.z_q_is + ((size_t)b * nq + (i - 1)) * FU_D * T);
+    if (tile_out) store_tile(a.z_q_is + ((size_t)b * nq + (i - 1)) * FU_D * T, a.nt_store != 0);
     FSTAMP(3);
     // (3) z_e, L2 normalisation (lane = f*8 + k; every wave of the group)
     float ze;
@@ -462,14 +466,22 @@ __global__ __launch_bounds__(FU_NT) void rvq_fused_kernel(FusedArgs a) {
     FSTAMP(7);
   }
   lds_barrier();
-  if (a.z_q_is) store_tile(a.z_q_is + ((size_t)b * nq + (nq - 1)) * FU_D * T);
+  if (a.z_q_is) store_tile(a.z_q_is + ((size_t)b * nq + (nq - 1)) * FU_D * T, a.nt_store != 0);
   lds_barrier();
 #pragma unroll
   for (int j = 0; j < FU_CPT; ++j)
 #pragma unroll
     for (int f = 0; f < FU_FPG; ++f) tile[(ct + 256 * j) * FU_TS + g * FU_FPG + f] = zacc[j][f];
   lds_barrier();
-  store_tile(a.z_q + (size_t)b * FU_D * T);
+  store_tile(a.z_q + (size_t)b * FU_D * T, false);  // re-read by the decoder
+}
+
+static int rvq_nt_store() {  // tuning override: VRVQ_RVQ_NT=0 (plain stores) | 1 (non-temporal)
+  static const int v = [] {
+    const char* e = getenv("VRVQ_RVQ_NT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -498,6 +510,7 @@ extern "C" int vrvq_rvq_fused(const float* z, int batch, int dim, int frames, in
   a.units = (int)units;
   a.per_xcd = (int)((units + 7) / 8);
   a.stamps = vrvq_g_stamps;
+  a.nt_store = rvq_nt_store();
   const dim3 grid((unsigned)(8 * a.per_xcd));
   hipStream_t st = as_stream(stream);
   switch (ncode / 256) {

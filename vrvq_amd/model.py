@@ -207,7 +207,29 @@ class ResidualVectorQuantize(nn.Module):
                 "commitment_loss": loss, "codebook_loss": loss.clone()}
 
     def from_codes(self, codes: torch.Tensor, return_z_q_is: bool = False):
-        raise NotImplementedError("from_codes (codes -> audio decode) is SURVEY.md §8f row 2")
+        """Codes -> continuous latents (models/quantize.py:217-249): per stage the raw codebook
+        row (decode_code, :81-85), out_proj, summed over the stages in order. Runs as two
+        launches: vrvq_rvq_gather (codes -> z_p rows) and vrvq_rvq_expand (out_proj + sum, no
+        gating). Returns (z_q, z_p, codes[, z_q_is]) like the reference."""
+        return self._from_codes(codes, return_z_q_is, None)
+
+    def _from_codes(self, codes, return_z_q_is, mask):
+        if not isinstance(codes, torch.Tensor) or codes.dim() != 3:
+            raise RuntimeError("from_codes: codes must be a (B, n_codebooks, T) tensor")
+        n = codes.shape[1]
+        if n > self.n_codebooks:  # the reference indexes self.quantizers[i]: IndexError
+            raise IndexError(f"{n} codebooks in codes, the model has {self.n_codebooks}")
+        st = self.stacked()
+        codes = codes.contiguous()
+        zst, z_p = ops.rvq_gather(codes, st.cb)
+        want_is = return_z_q_is or mask is not None
+        z_q_is, z_q, _ = ops.rvq_expand(zst, st.w_out[:n], st.b_out[:n], None, 1.0,
+                                        want_z_q_is=want_is, want_mask=False)
+        if mask is not None:
+            z_q = ops.masked_sum(z_q_is, mask.contiguous())
+        if return_z_q_is:
+            return z_q, z_p, codes, z_q_is
+        return z_q, z_p, codes
 
     def from_latents(self, latents: torch.Tensor):
         raise NotImplementedError("from_latents is outside the hot path (SURVEY.md §8f)")
@@ -272,8 +294,12 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
             "mask_imp": mask,
         }
 
-    def from_codes(self, codes: torch.Tensor, return_z_q_is=False):
-        raise NotImplementedError
+    def from_codes(self, codes: torch.Tensor, return_z_q_is=False, mask_imp=None):
+        """VBR codes -> z_q (the reference raises NotImplementedError at
+        models/quantize.py:445-446). Every stage's z_q_i as in ResidualVectorQuantize.from_codes;
+        with `mask_imp` (B, Nq, T) — the encode dict's mask — z_q is the masked sum of
+        scripts/inference.py:99-100, without it the plain sum over the given stages."""
+        return self._from_codes(codes, return_z_q_is, mask_imp)
 
     def from_latents(self, latents: torch.Tensor):
         raise NotImplementedError

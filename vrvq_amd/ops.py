@@ -221,6 +221,29 @@ def rvq_expand(zst, w_out, b_out, imp=None, level: float = 1.0, want_z_q_is: boo
     return z_q_is, z_q, mask
 
 
+def rvq_gather(codes: torch.Tensor, cb: torch.Tensor, want_zst: bool = True,
+               want_z_p: bool = True):
+    """decode_code of every stage (models/quantize.py:81-85): raw codebook rows for int64 codes
+    [B,nq,T] over the stacked codebooks cb [nq',N,d] (nq <= nq'). Returns (zst [B,nq,T,d],
+    z_p [B,nq*d,T]); an out-of-range code raises IndexError, as F.embedding does."""
+    _chk(codes, "codes", dtype=torch.int64); dev = codes.device
+    _chk(cb, "cb", device=dev)
+    if codes.dim() != 3:
+        raise RuntimeError("rvq_gather: codes must be (B, n_codebooks, T)")
+    B, nq, T = codes.shape
+    if nq > cb.shape[0]:
+        raise RuntimeError(f"rvq_gather: {nq} codebooks requested, {cb.shape[0]} available")
+    _, N, d = cb.shape
+    zst = torch.empty((B, nq, T, d), device=dev, dtype=torch.float32) if want_zst else None
+    z_p = torch.empty((B, nq * d, T), device=dev, dtype=torch.float32) if want_z_p else None
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    _lib.call("vrvq_rvq_gather", _p(codes), B, nq, T, _p(cb), N, d, _p(zst), _p(z_p), _p(err),
+              _stream(codes))
+    if int(err.item()) != 0:
+        raise IndexError(f"code out of range for codebook size {N}")
+    return zst, z_p
+
+
 def rvq_cross_prep(w_in_t, w_out, b_out):
     """M_ij = W_in[i] W_out[j] blocks (mcol [nq][nq][8][8]) and Qb [nq][8] of the projected
     chain (once per weight version)."""
