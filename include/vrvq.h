@@ -268,6 +268,27 @@ int vrvq_masked_sum(const float* z_q_is, const float* mask, int batch, int nq, i
 int vrvq_bpf(const float* mask, const float* bits, int batch, int nq, int frames, float* out,
              vrvq_stream_t stream);
 
+/* Variable-length code packing from importance masks (the reference's
+ * DACFile, models/dac_base.py:19-58, stores the full uint16 code matrix). Packed stream is
+ * clip-major, frame-major, stage-minor uint16: packed[clip_off[b] + frame_off[b,t] + i] =
+ * codes[b,i,t] for i < counts[b,t]; clip_off has B+1 entries (clip_off[B] = total codes).
+ *   vrvq_pack_counts     mask [B][nq][T] -> counts [B*T] (int32), clip_total [B], clip_off [B+1];
+ *                        *err = 1 if a mask column is not prefix-shaped (nq <= 255)
+ *   vrvq_pack_codes      codes [B][nq][T] int64 -> packed (clip_off[B] uint16); *err = 2 on a
+ *                        code outside [0, ncode)
+ *   vrvq_unpack_offsets  counts -> clip_total, clip_off (same scan as packing)
+ *   vrvq_unpack_codes    packed -> codes [B][nq][T] int64 (0 where masked) and mask or NULL */
+int vrvq_pack_counts(const float* mask, int batch, int nq, int frames, int* counts,
+                     long long* clip_total, long long* clip_off, int* err, vrvq_stream_t stream);
+int vrvq_pack_codes(const int64_t* codes, const int* counts, const long long* clip_off, int batch,
+                    int nq, int frames, int ncode, uint16_t* packed, int* err,
+                    vrvq_stream_t stream);
+int vrvq_unpack_offsets(const int* counts, int batch, int frames, long long* clip_total,
+                        long long* clip_off, vrvq_stream_t stream);
+int vrvq_unpack_codes(const uint16_t* packed, const int* counts, const long long* clip_off,
+                      int batch, int nq, int frames, int64_t* codes, float* mask,
+                      vrvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

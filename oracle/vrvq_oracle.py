@@ -279,3 +279,15 @@ def cal_bpf_from_mask(mask: np.ndarray, bits_per_codebook: List[float]) -> float
     """sum(mask * bits) / (B*T)   (models/utils.py:64-73)."""
     bits = np.asarray(bits_per_codebook, F32).reshape(1, -1, 1)
     return float(np.sum(mask * bits, dtype=np.float64) / (mask.shape[0] * mask.shape[2]))
+
+
+def pack_codes(codes: np.ndarray, mask: np.ndarray):
+    """Variable-length packing (vrvq_amd/codes_io.py; no reference
+    counterpart — the reference's DACFile, models/dac_base.py:19-58, stores every code): per
+    clip, per frame, the codes of the stages whose mask is 1, in stage order. Returns
+    (packed uint16, counts (B, T) int32)."""
+    B, nq, T = codes.shape
+    on = mask != 0
+    counts = on.sum(1).astype(np.int32)
+    packed = codes.transpose(0, 2, 1)[on.transpose(0, 2, 1)].astype(np.uint16)
+    return packed, counts

@@ -243,14 +243,30 @@ def from_codes_all(DAC, ref, manifest):
                        seed=6, vbr=True)
 
 
+def dac_file_fixture(ref_root):
+    """A .dac file written by the reference's own DACFile.save (models/dac_base.py:31-47)."""
+    from models.dac_base import DACFile
+    g = torch.Generator().manual_seed(3)
+    codes = torch.randint(0, 1024, (1, 8, 25), generator=g)
+    f = DACFile(codes=codes, chunk_length=25, original_length=12345,
+                input_db=torch.tensor([-17.25]), channels=1, sample_rate=44100, padding=True,
+                dac_version="1.0.0")
+    path = f.save(os.path.join(HERE, "ref_written"))
+    np.savez(os.path.join(HERE, "ref_written_expect.npz"), codes=codes.numpy())
+    print("dac file", path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.environ.get("VRVQ_REFERENCE", "/root/reference"))
-    ap.add_argument("--only", choices=["from_codes"], default=None,
+    ap.add_argument("--only", choices=["from_codes", "dac_file"], default=None,
                     help="regenerate only these fixtures and merge them into manifest.json")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
     DAC, ref_utils = load_ref(args.ref)
+    if args.only == "dac_file":
+        dac_file_fixture(args.ref)
+        return
     if args.only == "from_codes":
         with open(os.path.join(HERE, "manifest.json")) as f:
             manifest = json.load(f)
@@ -277,6 +293,7 @@ def main():
     rvq_stress_fixture(DAC, k32, "golden_rvq_stress_nq32", manifest, batch=2, frames=40, seed=11)
     mask_kat(ref_utils, manifest)
     from_codes_all(DAC, args.ref, manifest)
+    dac_file_fixture(args.ref)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, default=float)
 

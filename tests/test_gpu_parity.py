@@ -529,3 +529,70 @@ def test_encode_from_codes_roundtrip_full_batch(manifest):
                                                          mask_imp=enc["mask_imp"])
     assert rel_err(z_q.cpu().numpy(), enc["z_q"].cpu().numpy()) < TOL
     assert rel_err(z_q_is.cpu().numpy(), enc["z_q_is"].cpu().numpy()) < TOL
+
+
+# ------------------------------------------------------------------ variable-length code packing
+@pytest.mark.parametrize("B,nq,T", [(1, 8, 1), (3, 8, 87), (300, 8, 87), (2, 32, 1000),
+                                    (5, 28, 257)])
+def test_pack_codes_vs_oracle(B, nq, T):
+    """vrvq_pack_*  vs the numpy oracle: packed stream and counts bit-exact,
+    unpack restores the codes where the mask is 1 and the mask itself. Covers B > 256 (clip
+    scan carry), T > 256 (frame scan carry), empty and full frames."""
+    from oracle.vrvq_oracle import generate_mask_hard, pack_codes as pack_np
+    from vrvq_amd.codes_io import pack_codes, unpack_codes
+    rng = np.random.default_rng(B * 1000 + T)
+    codes = rng.integers(0, 1024, (B, nq, T)).astype(np.int64)
+    codes[0, :, 0] = 1023
+    s = (rng.random((B, 1, T)) * (nq + 2) - 1.0).astype(np.float32)
+    s[0, 0, 0] = nq           # full frame
+    if T > 1:
+        s[0, 0, 1] = -0.5     # empty frame
+    mask = generate_mask_hard(s, nq)
+    packed, counts = pack_codes(t(codes), t(mask))
+    want_p, want_c = pack_np(codes, mask)
+    np.testing.assert_array_equal(counts.cpu().numpy(), want_c)
+    np.testing.assert_array_equal(packed.cpu().numpy().view(np.uint16), want_p)
+    codes2, mask2 = unpack_codes(packed, counts, nq)
+    np.testing.assert_array_equal(mask2.cpu().numpy(), mask)
+    np.testing.assert_array_equal(codes2.cpu().numpy(), np.where(mask != 0, codes, 0))
+
+
+def test_pack_codes_errors_and_empty():
+    from vrvq_amd.codes_io import pack_codes, unpack_codes
+    codes = torch.zeros((2, 4, 10), dtype=torch.int64, device=DEV)
+    mask = torch.zeros((2, 4, 10), device=DEV)
+    packed, counts = pack_codes(codes, mask)
+    assert packed.numel() == 0 and int(counts.sum()) == 0
+    c2, m2 = unpack_codes(packed, counts, 4)
+    assert int(m2.sum()) == 0 and int(c2.abs().sum()) == 0
+    bad = mask.clone(); bad[0, 2, 3] = 1.0         # a 1 after a 0: not prefix-shaped
+    with pytest.raises(ValueError):
+        pack_codes(codes, bad)
+    ok = mask.clone(); ok[1, 0, 4] = 1.0
+    big = codes.clone(); big[1, 0, 4] = 1024
+    with pytest.raises(IndexError):
+        pack_codes(big, ok)
+    p, c = pack_codes(codes, ok)
+    with pytest.raises(ValueError):
+        unpack_codes(p, c, 0)                       # counts > n_codebooks
+
+
+def test_pack_roundtrip_full_batch_and_file(manifest, tmp_path):
+    """BASELINE batch 32: encode -> pack by mask_imp -> save/load -> unpack -> from_codes with
+    the unpacked mask reproduces the encode's z_q; packed size = bpf * B*T / 10."""
+    from vrvq_amd.codes_io import load_packed, pack_codes, save_packed, unpack_codes
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(32, 44100, seed=7))
+    with torch.no_grad():
+        enc = model.encode(model.preprocess(audio, 44100), None, 1.0)
+    packed, counts = pack_codes(enc["codes"], enc["mask_imp"])
+    bpf = vrvq_amd.cal_bpf_from_mask(enc["mask_imp"], [10] * 8)
+    assert packed.numel() == pytest.approx(bpf * counts.numel() / 10, abs=0.5)
+    path = save_packed(tmp_path / "clip", packed, counts, 8, sample_rate=44100)
+    p2, c2, meta = load_packed(path, device=DEV)
+    assert meta["n_codebooks"] == 8 and torch.equal(p2, packed) and torch.equal(c2, counts)
+    codes, mask = unpack_codes(p2, c2, 8)
+    assert torch.equal(mask, enc["mask_imp"])
+    with torch.no_grad():
+        z_q, _, _ = model.quantizer.from_codes(codes, mask_imp=mask)
+    assert rel_err(z_q.cpu().numpy(), enc["z_q"].cpu().numpy()) < TOL

@@ -46,6 +46,10 @@ SIGNATURES = {
     "vrvq_scale_imp": [_P, _I, _F, _F, _P, _P],
     "vrvq_masked_sum": [_P, _P, _I, _I, _I, _I, _P, _P],
     "vrvq_bpf": [_P, _P, _I, _I, _I, _P, _P],
+    "vrvq_pack_counts": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "vrvq_pack_codes": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "vrvq_unpack_offsets": [_P, _I, _I, _P, _P, _P],
+    "vrvq_unpack_codes": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
 }
 EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
          "vrvq_debug_set_stamps": ([_P], _I)}
