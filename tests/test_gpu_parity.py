@@ -152,6 +152,11 @@ CONV_CASES = [
     (2, 768, 768, 100, 7, 1, 27, 9, True, False, 0),
     (2, 512, 512, 96, 7, 1, 3, 1, True, False, 0),
     (1, 96, 8, 500, 7, 1, 3, 1, True, True, 2),
+    (1, 384, 384, 5000, 1, 1, 0, 1, True, True, 0),
+    (2, 768, 768, 696, 1, 1, 0, 1, True, True, 0),
+    (1, 384, 384, 700, 1, 1, 0, 1, True, True, 0),
+    (2, 512, 512, 696, 1, 1, 0, 1, True, True, 0),
+    (2, 768, 768, 696, 7, 1, 27, 9, True, False, 0),
 ]
 
 

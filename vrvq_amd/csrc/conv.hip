@@ -170,6 +170,26 @@ static int conv_bn_rule() {  // tuning override: VRVQ_CONV_BN_RULE=0 (minimise p
   return v;
 }
 
+// Measured (profiles/r01j_conv_k1_ab.txt): 768 x 768 k1 + skip at T = 696, 485 -> 386 us with
+// 192-row tiles (384: 930 -> 922 us); 256-row tiles for 512 / 768 were slower (248 / 473 us).
+static int conv_k1_192() {  // tuning override: VRVQ_CONV_K1_192=0 (128-row) | 1 (192-row, default)
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_K1_192");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// Measured (profiles/r01j_conv_k7_ab.txt): 768 x 768 k7 at T = 696, 2150 -> 1795 us with
+// 192-row x 64-col tiles (K chunk 4 channels), 427 -> 434 audio-sec/s end to end.
+static int conv_k7_192() {  // tuning override: VRVQ_CONV_K7_192=0 | 1 (192-row k7 tiles at BN 64,
+  static const int v = [] {  // default) | 2 (also at BN 128)
+    const char* e = getenv("VRVQ_CONV_K7_192");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -200,10 +220,22 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     if constexpr (kWide) if (wide) return launch_cfg<96, 256, 1, 8, KS>(a, batch, st);
     return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
   }
+  if (KS == 7 && conv_k7_192() && a.M % 192 == 0) {
+    if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
+    if (conv_k7_192() == 2) return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+  }
   if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
     // (KS == 2 with up > 0: the polyphase ConvTranspose1d 192->96 s2, M = 192 phase rows)
     if constexpr (kWide) if (wide) return launch_cfg<192, 256, 2, 8, KS>(a, batch, st);
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+  }
+  if constexpr (KS == 1) {
+    // k = 1 GEMMs with M a multiple of 192 (the 384 / 768-channel ResidualUnit k1 + skip):
+    // 192-row tiles read each x column block 2x / 4x instead of 3x / 6x (tuning knob)
+    if (conv_k1_192() && a.M % 192 == 0 && a.M % 128 == 0) {
+      if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
+      return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+    }
   }
   if (bn == 64) return launch_cfg<128, 64, 2, 4, KS>(a, batch, st);
   if constexpr (kWide) if (wide) return launch_cfg<128, 256, 2, 8, KS>(a, batch, st);
