@@ -190,6 +190,16 @@ static int conv_k7_192() {  // tuning override: VRVQ_CONV_K7_192=0 | 1 (192-row 
   return v;
 }
 
+// Measured (profiles/r01k_convt_ab.txt): ConvT 768->384 s8 2443 -> 2345 us, 384->192 s4
+// 2887 -> 2660 us with 192-row tiles; 432 -> 434 audio-sec/s.
+static int conv_t_192() {  // tuning override: VRVQ_CONVT_192=0 | 1 (192-row ConvT tiles, default)
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONVT_192");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -223,6 +233,11 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   if (KS == 7 && conv_k7_192() && a.M % 192 == 0) {
     if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     if (conv_k7_192() == 2) return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+  }
+  if (KS == 2 && a.up > 0 && conv_t_192() && a.M % 192 == 0) {
+    // polyphase ConvTranspose1d with M = Cout * stride phase rows a multiple of 192
+    if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
+    return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
   if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
     // (KS == 2 with up > 0: the polyphase ConvTranspose1d 192->96 s2, M = 192 phase rows)
