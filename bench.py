@@ -111,7 +111,7 @@ class RvqTimer:
     """HIP-event timing of the RVQ launch (vrvq_rvq_fused), recorded on the stream it runs
     on."""
 
-    KERNELS = ("fused",)
+    KERNELS = ("encode",)
 
     def __init__(self):
         self.events = []

@@ -116,7 +116,9 @@ int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channe
  * the DecoderBlock upsampler (models/layers.py:92-103): y has length tin*stride.
  * Computed as a polyphase 2-tap conv with cout*stride phase-channels:
  *   y[b,co,m*s+r-p] = bias[co] + sum_ci W[ci,co,r]*xs[ci,m] + W[ci,co,r+s]*xs[ci,m-1].
- * w_packed from vrvq_pack_convt1d_weight ([Cin][2][cout*stride padded to 128]).
+ * w_packed from vrvq_pack_convt1d_weight ([Cin][2][cout_pad]: cout*stride padded to a
+ * multiple of 128, or of 192 for strides that do not divide 128). Strides 5, 7, ... return
+ * VRVQ_ERR_UNSUPPORTED (a tile must hold whole output channels).
  * alpha_out / inv_alpha_out / y_snake: producer-side Snake as in vrvq_conv1d. */
 int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin, const float* alpha,
                           const float* inv_alpha, const float* w_packed, int cout,
@@ -202,28 +204,6 @@ int vrvq_rvq_fused(const float* z, int batch, int dim, int frames, int nq, int n
                    const float* c2, const float* w_out, const float* b_out, const float* imp,
                    float level, int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
                    float* z_q, float* mask, vrvq_stream_t stream);
-
-/* Channel-split single launch (vrvq_rvq_split): the outputs of vrvq_rvq_fused, computed by
- * groups of 8 workgroups that share one frame range (<= 64 frames of one clip); workgroup s of
- * a group owns latent channels [128 s, 128 s + 128) and codebook entries [s N/8, (s+1) N/8) and
- * exchanges the 8-dim in_proj partials and its argmin candidates with the group through L2
- * (two exchanges per stage, fixed summation / comparison order: every member computes the same
- * z_e and codes). Bit-identical to vrvq_rvq_codes + vrvq_rvq_expand except for the in_proj
- * partial-sum order. Replaces the same reference code as vrvq_rvq_fused
- * (models/quantize.py:353-365, 389-421).
- *   workspace  device buffer of at least vrvq_rvq_split_workspace() bytes, ZERO-FILLED before
- *              its first use; every launch leaves it zero again. Word 0 is an error flag: it
- *              becomes non-zero if a group exchange timed out (outputs invalid; the caller
- *              must zero the workspace again). One launch at a time per workspace.
- * Supported: D == 1024, d == 8, N % 256 == 0 and N <= 1024, D*T < 2^31, 16-byte aligned
- * weights and workspace. */
-int vrvq_rvq_split_workspace(int batch, int frames, long long* bytes);
-int vrvq_rvq_split(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
-                   const float* w_in_t, const float* b_in, const float* cb, const float* cbn,
-                   const float* c2, const float* w_out, const float* b_out, const float* imp,
-                   float level, int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
-                   float* z_q, float* mask, void* workspace, long long workspace_bytes,
-                   vrvq_stream_t stream);
 
 /* Stage 2 (vrvq_rvq_expand): HBM-streaming expansion + importance gating.
  *   z_q_is[b,i,:,t] = W_out[i] zst[b,i,t] + b_out[i]          (bit-identical to stage 1)

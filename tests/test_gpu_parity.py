@@ -198,7 +198,8 @@ def test_conv1d_vs_torch(case):
 
 
 @pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8), (2, 384, 192, 333, 4),
-                                  (2, 192, 96, 1000, 2), (1, 16, 8, 1, 2), (1, 64, 32, 3, 8)])
+                                  (2, 192, 96, 1000, 2), (1, 16, 8, 1, 2), (1, 64, 32, 3, 8),
+                                  (2, 64, 40, 77, 3), (1, 32, 16, 50, 6)])
 def test_conv_transpose1d_vs_torch(case):
     B, cin, cout, T, s = case
     gen = torch.Generator(device="cpu").manual_seed(s * 1000 + T)
@@ -221,6 +222,16 @@ def test_conv_transpose1d_vs_torch(case):
     assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
 
 
+def test_conv_transpose1d_unsupported_stride_raises():
+    """Strides whose phase rows cannot tile 128 or 192 rows (5, 7) are rejected, not computed
+    wrong (the epilogue maps whole output channels per tile)."""
+    x = torch.rand(1, 16, 20, device=DEV)
+    w = torch.rand(16, 8, 10, device=DEV)
+    wp, cout_pad = ops.pack_convt1d_weight(w, 5)
+    with pytest.raises(RuntimeError, match="instantiated kernel set"):
+        ops.conv_transpose1d(x, wp, 8, cout_pad, 5)
+
+
 def test_weight_norm_and_codebook_prep_vs_torch():
     gen = torch.Generator(device="cpu").manual_seed(5)
     v = torch.randn(300, 64, 7, generator=gen).to(DEV)
@@ -235,46 +246,98 @@ def test_weight_norm_and_codebook_prep_vs_torch():
     assert rel_err(c2.cpu().numpy(), rn.pow(2).sum(-1).cpu().numpy()) < 1e-6
 
 
-# ------------------------------------------------------------------ full-size properties
-def test_full_size_properties(manifest):
-    """BASELINE config 2 (B=32, 8 cb): size-independent invariants of the RVQ outputs, plus
-    oracle agreement on a frame subset."""
-    model = model_for(manifest, "golden_nq8")
-    audio = t(synthetic_audio(32, 44100, seed=4321))
-    with torch.no_grad():
-        x = model.preprocess(audio, 44100)
-        z, feat = model.encoder(x, return_feat=True)
-        out = model.quantizer(z, None, feat, 1)
-    codes, mask, zqis = out["codes"], out["mask_imp"], out["z_q_is"]
-    assert codes.shape == (32, 8, 87) and codes.min() >= 0 and codes.max() < 1024
-    assert torch.all(mask[:, 0] == 1)                               # s >= 0 always keeps codebook 0
-    assert torch.all(mask[:, 1:] <= mask[:, :-1])                   # monotone in codebook index
-    zq2 = vrvq_amd.masked_sum(zqis, mask)
-    assert torch.equal(zq2, out["z_q"])                             # same accumulation order
-    # oracle on two clips of the GPU's own latents
-    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **manifest["golden_nq8"]["kwargs"])
-    sel = [0, 31]
-    q = o.quantize(z[sel].cpu().numpy(), None, feat[sel].cpu().numpy(), 1.0)
-    np.testing.assert_array_equal(codes[sel].cpu().numpy(), q["codes"])
-    np.testing.assert_array_equal(mask[sel].cpu().numpy(), q["mask_imp"])
-    assert rel_err(out["z_q"][sel].cpu().numpy(), q["z_q"]) < TOL
+# ------------------------------------------------------------------ full-size parity
+# BASELINE.json configs at their full batch on the GPU, each compared clip by clip with the CPU
+# oracle run on that clip's own input (clips are independent through the whole path, so the
+# oracle on a subset equals the oracle on the batch, restricted to that subset). Codes and
+# masks bit-exact, z_q / audio / imp_map within 1e-4 (max-abs normalised).
+_full = {}
 
 
-def test_rvq_big_batch_nq32_vs_oracle(manifest):
-    """BASELINE config 3 shape (B=64, 32 cb) on random latents vs the oracle."""
-    model = model_for(manifest, "golden_nq32")
-    gen = torch.Generator(device="cpu").manual_seed(77)
-    z = torch.randn(64, 1024, 87, generator=gen) * 0.3
-    feat = torch.randn(64, 1024, 87, generator=gen) * 0.3
+def _full_run(manifest, name, B, nq=None, sel=(), seed=4321):
+    key = (name, B, nq, seed)
+    if key in _full:
+        return _full[key]
+    kw = dict(manifest[name]["kwargs"])
+    if nq is not None:
+        kw["n_codebooks"] = nq
+    model = vrvq_amd.DAC_VRVQ(**kw)
+    load_recipe(model, 0)
+    model = model.to(DEV).eval()
+    audio = synthetic_audio(B, 44100, seed=seed)
     with torch.no_grad():
-        out = model.quantizer(z.to(DEV), None, feat.to(DEV), 1)
-    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **manifest["golden_nq32"]["kwargs"])
-    q = o.quantize(z.numpy(), None, feat.numpy(), 1.0)
-    codes = out["codes"].cpu().numpy()
-    agree = (codes == q["codes"]).mean()
-    assert agree == 1.0, f"codes agreement {agree}"
-    np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), q["mask_imp"])
-    assert rel_err(out["z_q"].cpu().numpy(), q["z_q"]) < TOL
+        out = model(t(audio), 44100, None, 1)
+        enc = model.encode(model.preprocess(t(audio), 44100), None, 1)
+    torch.cuda.synchronize()
+    o = Oracle(recipe_state_dict(shapes_of(model.state_dict()), 0), **kw)
+    ref = o.forward(audio[list(sel)], None, 1.0)
+    _full[key] = (model, audio, out, enc, o, ref)
+    return _full[key]
+
+
+def _check_clips(out, enc, ref, sel):
+    sel = list(sel)
+    codes = out["codes"][sel].cpu().numpy()
+    bad = np.argwhere(codes != ref["codes"])
+    assert bad.size == 0, f"codes differ at (clip, stage, frame) {bad[:8].tolist()}"
+    np.testing.assert_array_equal(out["mask_imp"][sel].cpu().numpy(), ref["mask_imp"])
+    assert rel_err(out["imp_map"][sel].cpu().numpy(), ref["imp_map"]) < TOL
+    assert rel_err(out["latents"][sel].cpu().numpy(), ref["latents"]) < TOL
+    assert rel_err(out["z"][sel].cpu().numpy(), ref["z_q"]) < TOL
+    assert rel_err(out["audio"][sel].cpu().numpy(), ref["audio"]) < TOL
+    zqis = enc["z_q_is"][sel].cpu().numpy()
+    assert rel_err(zqis, ref["z_q_is"]) < TOL
+    # batch-level invariants over every clip
+    mask = out["mask_imp"]
+    assert torch.all(mask[:, 0] == 1) and torch.all(mask[:, 1:] <= mask[:, :-1])
+    assert torch.equal(vrvq_amd.masked_sum(enc["z_q_is"], enc["mask_imp"]), enc["z_q"])
+
+
+CFG2_CLIPS = (0, 5, 9, 14, 18, 23, 27, 31)
+
+
+def test_config2_full_batch_vs_oracle(manifest):
+    """BASELINE config 2: conf/base.yml (8 cb VBR), B = 32 x 1 s, level 1: 8 clips spread over
+    the batch vs the oracle (models/dac_vrvq.py:222-252)."""
+    _model, _a, out, enc, _o, ref = _full_run(manifest, "golden_nq8", 32, sel=CFG2_CLIPS)
+    assert out["codes"].shape == (32, 8, 87) and out["audio"].shape == (32, 1, 44100)
+    _check_clips(out, enc, ref, CFG2_CLIPS)
+
+
+@pytest.mark.parametrize("nq", [28, 32])
+def test_config3_full_batch_vs_oracle(manifest, nq):
+    """BASELINE config 3: conf/base_24kbps.yml (n_codebooks 28 as in the file, and the 32
+    override), B = 64, whole model: 4 clips spread over the batch vs the oracle."""
+    sel = (0, 21, 42, 63)
+    _model, _a, out, enc, _o, ref = _full_run(manifest, "golden_nq28", 64, nq=nq, sel=sel, seed=77)
+    assert out["codes"].shape == (64, nq, 87)
+    _check_clips(out, enc, ref, sel)
+
+
+def test_level_sweep_full_batch_vs_oracle(manifest):
+    """scripts/inference.py:88-112 at B = 32 (BASELINE config 5's per-GPU shape x2): for every
+    level, masks bit-exact and z_q within 1e-4 on the 8 oracle clips, recon of 2 clips vs the
+    oracle decoder, bpf / kbps over the whole batch equal to the reference formula on the
+    masks (models/utils.py:64-73) and, over the oracle clips, to the oracle's own bpf."""
+    from oracle.vrvq_oracle import cal_bpf_from_mask as bpf_np, generate_mask_hard as mask_np
+    from oracle.vrvq_oracle import masked_sum as msum_np
+    model, audio, _out, _enc, o, ref = _full_run(manifest, "golden_nq8", 32, sel=CFG2_CLIPS)
+    res = vrvq_amd.level_sweep(model, t(audio), manifest["levels"])
+    sel = list(CFG2_CLIPS)
+    nq = model.n_codebooks
+    for r in res:
+        lv = float(r["level"])
+        s = (ref["imp_map"] * np.float32(lv * nq)).astype(np.float32)
+        m_ref = mask_np(s, nq)
+        mask = r["mask"].cpu().numpy()
+        np.testing.assert_array_equal(mask[sel], m_ref)
+        assert rel_err(r["z_q"][sel].cpu().numpy(), msum_np(ref["z_q_is"], m_ref)) < TOL
+        y = o.decoder(msum_np(ref["z_q_is"][:2], m_ref[:2]))
+        assert rel_err(r["recon"][sel[:2]].cpu().numpy(), y) < TOL
+        assert r["bpf"] == pytest.approx(bpf_np(mask, [10] * nq), rel=1e-6)
+        assert r["kbps"] == pytest.approx(r["bpf"] * 86 / 1000, rel=1e-12)
+        sub = vrvq_amd.cal_bpf_from_mask(r["mask"][sel].contiguous(), [10] * nq)
+        assert sub == pytest.approx(bpf_np(m_ref, [10] * nq), rel=1e-6)
 
 
 @pytest.mark.parametrize("length", [1, 511, 512, 513, 3000])
@@ -311,7 +374,7 @@ def test_cbr_mode_of_vbr_model(manifest):
             model.encode(x, n_quantizers=4)
 
 
-# ------------------------------------------------------------------ single-launch RVQ kernel
+# ------------------------------------------------------------------ RVQ operator
 def _rvq_fp64_reference(z, st, imp, level):
     """Plain PyTorch fp64 restatement of the RVQ chain + gating (models/quantize.py:42-103,
     353-421; models/utils.py:55-61) on the kernels' stacked weights."""
@@ -345,78 +408,58 @@ def _rvq_fp64_reference(z, st, imp, level):
     return codes, z_q_is, z_q, mask
 
 
-@pytest.mark.parametrize("path", ["encode", "fused", "split"])
-@pytest.mark.parametrize("nq,ncode,B,T,vbr", [
-    (8, 1024, 3, 87, True), (8, 1024, 2, 1, True), (8, 1024, 2, 13, True), (8, 1024, 1, 25, False),
-    (1, 1024, 4, 87, False), (32, 1024, 2, 87, True), (4, 256, 3, 40, True), (4, 512, 2, 87, True),
-    (4, 768, 2, 12, False), (28, 1024, 2, 70, True)])
-def test_rvq_paths_vs_fp64_and_two_kernel(path, nq, ncode, B, T, vbr):
-    """The production RVQ path (vrvq_rvq_project -> vrvq_rvq_chain -> vrvq_rvq_expand) and the
-    single-launch vrvq_rvq_fused against a torch fp64 reference and against the two-kernel
-    1024-dim chain (vrvq_rvq_codes + vrvq_rvq_expand): every codebook size variant
-    (N/256 = 1..4), frame ranges that are partial (T = 1, 13, 25, 40, 70) or exact (12),
-    nq = 1 .. 32, VBR and CBR."""
-    gen = torch.Generator().manual_seed(1000 * nq + T)
+def _random_rvq(nq, ncode, seed):
+    gen = torch.Generator().manual_seed(seed)
     q = vrvq_amd.model.ResidualVectorQuantize(input_dim=1024, n_codebooks=nq, codebook_size=ncode,
                                               codebook_dim=8)
     with torch.no_grad():
         for p in q.parameters():
             p.copy_(torch.randn(p.shape, generator=gen) * (0.05 if p.ndim == 3 else 1.0))
-    q = q.to(DEV).eval()
+    return q.to(DEV).eval(), gen
+
+
+@pytest.mark.parametrize("nq,ncode,B,T,vbr", [
+    (8, 1024, 3, 87, True), (8, 1024, 2, 1, True), (8, 1024, 2, 13, True), (8, 1024, 1, 25, False),
+    (1, 1024, 4, 87, False), (32, 1024, 2, 87, True), (4, 256, 3, 40, True), (4, 512, 2, 87, True),
+    (4, 768, 2, 12, False), (28, 1024, 2, 70, True), (8, 1024, 5, 200, True)])
+def test_rvq_encode_vs_fp64(nq, ncode, B, T, vbr):
+    """torch.ops.vrvq.rvq_encode against a torch fp64 reference: every codebook size variant
+    (N/256 = 1..4), partial and exact frame ranges, nq = 1 .. 32, VBR and CBR; z_q_is also
+    against the codes -> rows -> out_proj path (rvq_gather + rvq_expand)."""
+    q, gen = _random_rvq(nq, ncode, 1000 * nq + T)
     st = q.stacked()
     z = (torch.randn(B, 1024, T, generator=gen) * 0.3).to(DEV)
     imp = torch.rand(B, T, generator=gen).to(DEV) if vbr else None
     level = 0.75
-    if path == "encode":
-        codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=level)
-    elif path == "split":
-        codes, lat, loss, zqis, zq, mask = ops.rvq_split(z, *st.codes_args(), imp=imp, level=level)
-        assert not ops.rvq_split_error(z.device)
-    else:
-        codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=level)
-    c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())
-    zqis2, zq2, mask2 = ops.rvq_expand(zst, st.w_out, st.b_out, imp, level)
+    codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=level)
     torch.cuda.synchronize()
     rc, rzqis, rzq, rmask = _rvq_fp64_reference(z, st, imp, level)
     assert (codes.cpu() == rc).float().mean().item() == 1.0
-    assert torch.equal(codes, c2)
     np.testing.assert_array_equal(mask.cpu().numpy(), rmask.numpy())
-    assert torch.equal(mask, mask2)
     assert rel_err(zqis.cpu().numpy(), rzqis.numpy()) < 1e-5
     assert rel_err(zq.cpu().numpy(), rzq.numpy()) < 1e-5
+    zst, _ = ops.rvq_gather(codes, st.cb)
+    zqis2, _, _ = ops.rvq_expand(zst, st.w_out, st.b_out)
     assert rel_err(zqis.cpu().numpy(), zqis2.cpu().numpy()) < 1e-5
-    assert rel_err(lat.cpu().numpy(), lat2.cpu().numpy()) < 1e-5
-    assert rel_err(loss.cpu().numpy(), loss2.cpu().numpy()) < 1e-4
-    # the masked sum of the path's own z_q_is, in stage order, is its z_q bit for bit
+    # latents are the z_e of each stage; the loss is mean_k (z_e - z_q)^2 (models/quantize.py:69-71)
+    zrows = zst.permute(0, 1, 3, 2).reshape(B, nq * 8, T)
+    ref_loss = (lat - zrows).pow(2).reshape(B, nq, 8, T).mean(2)
+    assert rel_err(loss.cpu().numpy(), ref_loss.cpu().numpy()) < 1e-4
+    # the masked sum of the op's own z_q_is, in stage order, is its z_q bit for bit
     assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)
 
 
-@pytest.mark.parametrize("path", ["encode", "fused", "split"])
-def test_rvq_big_batch_properties(path):
-    """BASELINE config 3 shape (B=64, 32 codebooks): two rounds of workgroups per CU."""
-    gen = torch.Generator().manual_seed(5)
-    q = vrvq_amd.model.ResidualVectorQuantize(input_dim=1024, n_codebooks=32, codebook_size=1024,
-                                              codebook_dim=8)
-    with torch.no_grad():
-        for p in q.parameters():
-            p.copy_(torch.randn(p.shape, generator=gen) * (0.05 if p.ndim == 3 else 1.0))
-    q = q.to(DEV).eval()
+def test_rvq_big_batch_nq32_properties():
+    """BASELINE config 3 shape (B=64, 32 codebooks) on random weights: fp64 codes agreement
+    and the invariants at full size."""
+    q, gen = _random_rvq(32, 1024, 5)
     st = q.stacked()
     z = (torch.randn(64, 1024, 87, generator=gen) * 0.3).to(DEV)
     imp = torch.rand(64, 87, generator=gen).to(DEV)
-    if path == "encode":
-        codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, st, imp=imp, level=1.0)
-    elif path == "split":
-        codes, lat, loss, zqis, zq, mask = ops.rvq_split(z, *st.codes_args(), imp=imp, level=1.0)
-        assert not ops.rvq_split_error(z.device)
-    else:
-        codes, lat, loss, zqis, zq, mask = ops.rvq_fused(z, *st.codes_args(), imp=imp, level=1.0)
-    c2, lat2, loss2, zst = ops.rvq_codes(z, *st.codes_args())
-    zqis2, zq2, mask2 = ops.rvq_expand(zst, st.w_out, st.b_out, imp, 1.0)
-    assert (codes == c2).float().mean().item() > 0.999
-    assert torch.equal(mask, mask2)
-    ok = (codes == c2).all(1).all(1)  # clips whose chains agree everywhere
-    assert rel_err(zqis[ok].cpu().numpy(), zqis2[ok].cpu().numpy()) < 1e-6
+    codes, lat, loss, zqis, zq, mask = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+    rc, rzqis, rzq, rmask = _rvq_fp64_reference(z[:4], st, imp[:4], 1.0)
+    assert torch.equal(codes[:4].cpu(), rc)
+    assert rel_err(zqis[:4].cpu().numpy(), rzqis.numpy()) < 1e-5
     assert torch.all(mask[:, 1:] <= mask[:, :-1])
     assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)
 

@@ -37,9 +37,6 @@ SIGNATURES = {
                        _P],
     "vrvq_rvq_fused": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P,
                        _P, _P, _P, _P],
-    "vrvq_rvq_split_workspace": [_I, _I, _P],
-    "vrvq_rvq_split": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P,
-                       _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_rvq_gather": [_P, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P],
     "vrvq_masked_loss": [_P, _P, _I, _I, _I, _P, _P],
     "vrvq_mask_hard": [_P, _I, _I, _I, _P, _P],

@@ -1,5 +1,10 @@
-"""Build libvrvq_hip.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the
-repo snapshot to the GPU box)."""
+"""Build the two in-tree libraries with hipcc for gfx950 (no JIT cache: the .so files travel
+with the repo snapshot to the GPU box):
+
+  libvrvq_hip.so    the HIP kernels + the C-ABI of include/vrvq.h (no torch dependency)
+  libvrvq_torch.so  TORCH_LIBRARY(vrvq) custom operators (csrc/torch_ops.cpp, host code only)
+                    over that C-ABI, loaded with torch.ops.load_library
+"""
 from __future__ import annotations
 
 import glob
@@ -12,6 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvrvq_hip.so")
+TORCH_LIB = os.path.join(HERE, "libvrvq_torch.so")
+TORCH_SRC = os.path.join(CSRC, "torch_ops.cpp")
 ARCH = os.environ.get("VRVQ_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs independent fp32 chains into v_pk_* with extra
 # v_mov shuffles and +40 VGPRs in the RVQ kernel; packed math is written explicitly instead.
@@ -29,11 +36,15 @@ def deps():
         os.path.join(REPO, "include", "vrvq.h"), os.path.abspath(__file__)]
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+def _newer(out: str, inputs) -> bool:
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(d) <= t for d in deps())
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(d) <= t for d in inputs)
+
+
+def up_to_date() -> bool:
+    return _newer(LIB, deps()) and _newer(TORCH_LIB, [TORCH_SRC, LIB] + deps())
 
 
 def hipcc() -> str:
@@ -63,16 +74,42 @@ def _compile_and_link(out: str, extra, verbose: bool, tag: str) -> str:
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
     tmp = out + ".tmp"
-    subprocess.run([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs,
-                   check=True)
+    subprocess.run([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}",
+                    f"-Wl,-soname,{os.path.basename(out)}", "-o", tmp] + objs, check=True)
     os.replace(tmp, out)
     return out
 
 
+def build_torch_ops(verbose: bool = True) -> str:
+    """libvrvq_torch.so: the TORCH_LIBRARY registration (host-only C++ against the torch ROCm
+    headers), linked to libvrvq_hip.so through an $ORIGIN rpath."""
+    from torch.utils import cpp_extension as ce
+    import torch
+
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    inc = sum((["-I", p] for p in ce.include_paths()), [])
+    tlib = ce.library_paths()[0]
+    tmp = TORCH_LIB + ".tmp"
+    cmd = [hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-variable",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           *inc, "-I", os.path.join(REPO, "include"), TORCH_SRC, "-o", tmp,
+           "-L", HERE, "-lvrvq_hip", "-L", tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+           "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{tlib}", "-Wl,-soname,libvrvq_torch.so"]
+    if verbose:
+        print("[vrvq_amd] " + " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, TORCH_LIB)
+    return TORCH_LIB
+
+
 def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
-        return LIB
-    return _compile_and_link(LIB, [], verbose, "")
+    if not force and _newer(LIB, deps()):
+        pass
+    else:
+        _compile_and_link(LIB, [], verbose, "")
+    if force or not _newer(TORCH_LIB, [TORCH_SRC, LIB] + deps()):
+        build_torch_ops(verbose)
+    return LIB
 
 
 def build_stamped(verbose: bool = True) -> str:

@@ -21,10 +21,10 @@ from typing import Tuple
 import numpy as np
 import torch
 
-from . import _lib
-from .ops import _chk, _p, _stream
+from .ops import _ops
 
 SUPPORTED_VERSIONS = ["1.0.0"]
+MAX_CODEBOOKS = 255  # counts are stored as uint8 (save_packed)
 
 
 # ----------------------------------------------------------------------------- GPU packing
@@ -32,51 +32,43 @@ def pack_codes(codes: torch.Tensor, mask: torch.Tensor, codebook_size: int = 102
                ) -> Tuple[torch.Tensor, torch.Tensor]:
     """codes (B, Nq, T) int64 + prefix-shaped mask (B, Nq, T) -> (packed uint16 stream as int16
     storage, counts (B, T) int32). Raises ValueError for a non-prefix mask column and
-    IndexError for a code outside [0, codebook_size)."""
-    _chk(codes, "codes", dtype=torch.int64); dev = codes.device
-    _chk(mask, "mask", device=dev)
+    IndexError for a code outside [0, codebook_size). The packed length is data-dependent, so
+    this synchronises the host once (like torch.nonzero)."""
     if codes.dim() != 3 or mask.shape != codes.shape:
         raise RuntimeError("pack_codes: codes and mask must both be (B, Nq, T)")
-    B, nq, T = codes.shape
-    counts = torch.empty((B, T), device=dev, dtype=torch.int32)
-    tot = torch.empty(B, device=dev, dtype=torch.int64)
-    off = torch.empty(B + 1, device=dev, dtype=torch.int64)
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
-    st = _stream(codes)
-    _lib.call("vrvq_pack_counts", _p(mask), B, nq, T, _p(counts), _p(tot), _p(off), _p(err), st)
+    if codes.shape[1] > MAX_CODEBOOKS:
+        raise ValueError(f"pack_codes: at most {MAX_CODEBOOKS} codebooks")
+    counts, off, err = _ops().pack_counts(mask)
+    B = codes.shape[0]
     total = int(off[B].item())
     if int(err.item()) == 1:
         raise ValueError("pack_codes: mask is not prefix-shaped (a 1 after a 0 along Nq)")
-    packed = torch.empty(max(total, 1), device=dev, dtype=torch.int16)[:total]
-    if total:
-        _lib.call("vrvq_pack_codes", _p(codes), _p(counts), _p(off), B, nq, T,
-                  int(codebook_size), _p(packed), _p(err), st)
-        if int(err.item()) == 2:
-            raise IndexError(f"pack_codes: code outside [0, {codebook_size})")
+    packed, err2 = _ops().pack_codes(codes, counts, off, total, int(codebook_size))
+    if total and int(err2.item()) == 2:
+        raise IndexError(f"pack_codes: code outside [0, {codebook_size})")
     return packed, counts
 
 
 def unpack_codes(packed: torch.Tensor, counts: torch.Tensor, n_codebooks: int
                  ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Inverse of pack_codes: -> codes (B, Nq, T) int64 (0 where masked), mask (B, Nq, T)."""
-    _chk(counts, "counts", dtype=torch.int32); dev = counts.device
-    _chk(packed, "packed", dtype=torch.int16, device=dev)
-    B, T = counts.shape
+    """Inverse of pack_codes: -> codes (B, Nq, T) int64 (0 where masked), mask (B, Nq, T).
+    n_codebooks must be the value the stream was packed with (load_packed returns it in the
+    metadata); a stream whose counts exceed it, or whose length disagrees with the counts,
+    raises ValueError."""
+    if not 0 < int(n_codebooks) <= MAX_CODEBOOKS:
+        raise ValueError(f"unpack_codes: n_codebooks must be in [1, {MAX_CODEBOOKS}]")
+    if packed.dim() != 1:
+        raise ValueError("unpack_codes: packed must be a 1-D stream")
+    if counts.dim() != 2:
+        raise ValueError("unpack_codes: counts must be (B, T)")
     if int(counts.min()) < 0 or int(counts.max()) > n_codebooks:
         raise ValueError(f"unpack_codes: counts outside [0, {n_codebooks}]")
-    tot = torch.empty(B, device=dev, dtype=torch.int64)
-    off = torch.empty(B + 1, device=dev, dtype=torch.int64)
-    st = _stream(counts)
-    _lib.call("vrvq_unpack_offsets", _p(counts), B, T, _p(tot), _p(off), st)
+    off = _ops().unpack_offsets(counts)
+    B = counts.shape[0]
     if int(off[B].item()) != packed.numel():
         raise ValueError(f"unpack_codes: stream holds {packed.numel()} codes, counts say "
                          f"{int(off[B].item())}")
-    codes = torch.empty((B, n_codebooks, T), device=dev, dtype=torch.int64)
-    mask = torch.empty((B, n_codebooks, T), device=dev, dtype=torch.float32)
-    src = packed if packed.numel() else torch.zeros(1, device=dev, dtype=torch.int16)
-    _lib.call("vrvq_unpack_codes", _p(src), _p(counts), _p(off), B, n_codebooks, T, _p(codes),
-              _p(mask), st)
-    return codes, mask
+    return _ops().unpack_codes(packed, counts, off, int(n_codebooks))
 
 
 def save_packed(path, packed: torch.Tensor, counts: torch.Tensor, n_codebooks: int,

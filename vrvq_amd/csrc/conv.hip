@@ -133,6 +133,9 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   a.n_mt = (a.M + BM - 1) / BM;
   a.n_nt = (a.ng + BN - 1) / BN;
   if (a.m_pad < a.n_mt * BM) return VRVQ_ERR_ARG;
+  // transposed conv: a tile must hold whole output channels (rows co*up .. co*up + up-1), the
+  // epilogue maps rows back with co0 = m0 / up
+  if (a.up > 0 && BM % a.up != 0) return VRVQ_ERR_UNSUPPORTED;
   constexpr int CK = ChunkCfg<KS, BM>::CK;
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
   const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
@@ -215,6 +218,13 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   else if (a.ng < 4096 && conv_bn_rule() == 0 && waste(64) * 10 < waste(128) * 7) bn = 64;
   else if (a.ng < 4096 && conv_bn_rule() == 1 && waste(128) * 100 > a.ng * 15) bn = 64;
   else bn = 128;
+  if (KS == 2 && a.up > 0 && 128 % a.up != 0) {
+    // polyphase ConvTranspose1d with a stride that does not divide 128 (3, 6): 192-row tiles,
+    // which hold whole output channels; other strides (5, 7, ...) are rejected by launch_cfg
+    if (bn <= 96 && bn != 64) bn = 64;
+    if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
+    return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
+  }
   if (a.M <= 32) return launch_cfg<32, 128, 1, 4, KS>(a, batch, st);
   if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
   if (bn == 96) return launch_cfg<128, 96, 4, 4, KS>(a, batch, st);
@@ -345,7 +355,7 @@ extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin
   VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
   VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && stride > 0);
-  VRVQ_CHECK_ARG(cout_pad >= cout * stride && cout_pad % 128 == 0);
+  VRVQ_CHECK_ARG(cout_pad >= cout * stride && cout_pad % 64 == 0);
   VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
   const int p = (stride + 1) / 2;  // math.ceil(stride / 2), models/layers.py:102
   ConvArgs a{};

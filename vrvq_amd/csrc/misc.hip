@@ -143,31 +143,33 @@ unsigned grid_for(size_t total, unsigned block) {
 // ResidualVectorQuantize.from_codes, :217-249): z_p[b, i*d + k, t] = cb[i][codes[b,i,t]][k]
 // (raw, un-normalised rows) in the reference's latents layout, plus the same rows as
 // zst[b][i][t][d], the input layout of vrvq_rvq_expand (out_proj + masked sum). One thread per
-// (b, i, t); consecutive t -> consecutive lanes, so the z_p row stores coalesce.
+// (b, i, t) (grid-stride: any B*nq*T); consecutive t -> consecutive lanes, so the z_p row
+// stores coalesce.
 __global__ __launch_bounds__(256) void rvq_gather_kernel(const int64_t* __restrict__ codes,
                                                          const float* __restrict__ cb, int batch,
                                                          int nq, int frames, int ncode, int cdim,
                                                          float* __restrict__ zst,
                                                          float* __restrict__ z_p,
                                                          int* __restrict__ err) {
-  const size_t n = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t total = (size_t)batch * nq * frames;
-  if (n >= total) return;
-  const int t = (int)(n % frames);
-  const size_t bi = n / frames;            // b * nq + i
-  const int i = (int)(bi % nq);
-  long long c = codes[n];
-  if (c < 0 || c >= ncode) {               // F.embedding raises IndexError; report, read row 0
-    if (err) *err = 1;
-    c = 0;
-  }
-  const float* row = cb + ((size_t)i * ncode + (size_t)c) * cdim;
-  float* zs = zst ? zst + n * cdim : nullptr;
-  float* zp = z_p ? z_p + bi * cdim * frames + t : nullptr;
-  for (int k = 0; k < cdim; ++k) {
-    const float v = row[k];
-    if (zs) zs[k] = v;
-    if (zp) zp[(size_t)k * frames] = v;
+  for (size_t n = (size_t)blockIdx.x * blockDim.x + threadIdx.x; n < total;
+       n += (size_t)gridDim.x * blockDim.x) {
+    const int t = (int)(n % frames);
+    const size_t bi = n / frames;            // b * nq + i
+    const int i = (int)(bi % nq);
+    long long c = codes[n];
+    if (c < 0 || c >= ncode) {               // F.embedding raises IndexError; report, read row 0
+      if (err) *err = 1;
+      c = 0;
+    }
+    const float* row = cb + ((size_t)i * ncode + (size_t)c) * cdim;
+    float* zs = zst ? zst + n * cdim : nullptr;
+    float* zp = z_p ? z_p + bi * cdim * frames + t : nullptr;
+    for (int k = 0; k < cdim; ++k) {
+      const float v = row[k];
+      if (zs) zs[k] = v;
+      if (zp) zp[(size_t)k * frames] = v;
+    }
   }
 }
 

@@ -1,0 +1,568 @@
+// PyTorch-ROCm custom operators over the C-ABI of libvrvq_hip.so (include/vrvq.h).
+//
+// TORCH_LIBRARY(vrvq, m) registers the hot-path operators as `torch.ops.vrvq.*`, with
+// implementations on the CUDA (= HIP on ROCm) dispatch key. Every op:
+//   - checks its tensors (device, fp32 / int dtype, contiguity) with TORCH_CHECK, so misuse is
+//     a Python RuntimeError, and a C-ABI status != 0 becomes a RuntimeError with its text;
+//   - allocates outputs with the torch caching allocator (at::empty) and launches on the
+//     current HIP stream of the input's device (c10::hip::getCurrentHIPStream), so ops are
+//     stream-ordered and capturable in a torch.cuda.CUDAGraph (no host sync, no hipMalloc);
+//   - returns an empty (0-element) tensor for an output the caller did not request (the Python
+//     wrappers in vrvq_amd/ops.py turn those into None).
+// Fake (meta) implementations for shape propagation live in vrvq_amd/ops.py
+// (torch.library.register_fake). Each op cites the reference operator it replaces.
+#include <ATen/core/Tensor.h>
+#include <ATen/ops/empty.h>
+#include <ATen/ops/empty_like.h>
+#include <ATen/ops/zeros.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "../../include/vrvq.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+void* stream_of(const Tensor& t) {
+  return reinterpret_cast<void*>(c10::hip::getCurrentHIPStream(t.device().index()).stream());
+}
+
+void check_rc(int rc, const char* fn) {
+  TORCH_CHECK(rc == 0, fn, " failed (", rc, "): ", vrvq_status_string(rc));
+}
+
+void check_t(const Tensor& t, const char* name, at::ScalarType dt = at::kFloat) {
+  TORCH_CHECK(t.is_cuda(), name, ": vrvq kernels run on the GPU only (got device ", t.device(),
+              ")");
+  TORCH_CHECK(t.scalar_type() == dt, name, ": expected ", dt, ", got ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, ": tensor must be contiguous");
+}
+
+void check_on(const Tensor& t, const Tensor& ref, const char* name,
+              at::ScalarType dt = at::kFloat) {
+  check_t(t, name, dt);
+  TORCH_CHECK(t.device() == ref.device(), name, ": on ", t.device(), ", expected ",
+              ref.device());
+}
+
+const float* fp(const optional<Tensor>& t) {
+  return t.has_value() ? t->data_ptr<float>() : nullptr;
+}
+
+void check_opt(const optional<Tensor>& t, const Tensor& ref, const char* name) {
+  if (t.has_value()) check_on(*t, ref, name);
+}
+
+Tensor empty_f(at::IntArrayRef shape, const Tensor& like) {
+  return at::empty(shape, like.options().dtype(at::kFloat));
+}
+
+Tensor none_like(const Tensor& like) { return at::empty({0}, like.options()); }
+
+int64_t round_up(int64_t n, int64_t m) { return (n + m - 1) / m * m; }
+
+// --------------------------------------------------------------------------- weights
+// torch.nn.utils.weight_norm(dim=0), models/layers.py:17-22.
+Tensor weight_norm(const Tensor& g, const Tensor& v) {
+  check_t(g, "g");
+  check_on(v, g, "v");
+  c10::DeviceGuard guard(v.device());
+  const int64_t rows = v.size(0), cols = v.numel() / rows;
+  TORCH_CHECK(g.numel() == rows, "weight_norm: g must have one entry per row of v");
+  Tensor w = at::empty_like(v);
+  check_rc(vrvq_weight_norm(g.data_ptr<float>(), v.data_ptr<float>(), (int)rows, (int)cols,
+                            w.data_ptr<float>(), stream_of(v)),
+           "vrvq_weight_norm");
+  return w;
+}
+
+// 1 / (alpha + 1e-9), models/layers.py:30.
+Tensor snake_inv_alpha(const Tensor& alpha) {
+  check_t(alpha, "alpha");
+  c10::DeviceGuard guard(alpha.device());
+  Tensor inv = at::empty_like(alpha);
+  check_rc(vrvq_snake_inv_alpha(alpha.data_ptr<float>(), (int)alpha.numel(),
+                                inv.data_ptr<float>(), stream_of(alpha)),
+           "vrvq_snake_inv_alpha");
+  return inv;
+}
+
+// F.normalize of the codebook rows + squared norms, models/quantize.py:92-99.
+std::tuple<Tensor, Tensor> codebook_prep(const Tensor& cb) {
+  check_t(cb, "codebook");
+  c10::DeviceGuard guard(cb.device());
+  const int64_t dim = cb.size(-1), rows = cb.numel() / dim;
+  Tensor cbn = at::empty_like(cb);
+  Tensor c2 = empty_f(cb.sizes().slice(0, cb.dim() - 1), cb);
+  check_rc(vrvq_codebook_prep(cb.data_ptr<float>(), (int)rows, (int)dim, cbn.data_ptr<float>(),
+                              c2.data_ptr<float>(), stream_of(cb)),
+           "vrvq_codebook_prep");
+  return {cbn, c2};
+}
+
+Tensor pack_conv1d_weight(const Tensor& w) {
+  check_t(w, "w");
+  TORCH_CHECK(w.dim() == 3, "pack_conv1d_weight: w must be (Cout, Cin, k)");
+  c10::DeviceGuard guard(w.device());
+  const int64_t cout = w.size(0), cin = w.size(1), k = w.size(2);
+  const int64_t cout_pad = round_up(cout, 128);
+  Tensor wp = empty_f({cin, k, cout_pad}, w);
+  check_rc(vrvq_pack_conv1d_weight(w.data_ptr<float>(), (int)cout, (int)cin, (int)k,
+                                   (int)cout_pad, wp.data_ptr<float>(), stream_of(w)),
+           "vrvq_pack_conv1d_weight");
+  return wp;
+}
+
+Tensor pack_convt1d_weight(const Tensor& w, int64_t stride) {
+  check_t(w, "w");
+  TORCH_CHECK(w.dim() == 3, "pack_convt1d_weight: w must be (Cin, Cout, k)");
+  TORCH_CHECK(w.size(2) == 2 * stride,
+              "conv_transpose1d: kernel_size must be 2*stride (DecoderBlock)");
+  c10::DeviceGuard guard(w.device());
+  const int64_t cin = w.size(0), cout = w.size(1);
+  // phase rows padded to whole 128-row tiles, or 192-row tiles for strides not dividing 128
+  const int64_t cout_pad = round_up(cout * stride, 128 % stride == 0 ? 128 : 192);
+  Tensor wp = empty_f({cin, 2, cout_pad}, w);
+  check_rc(vrvq_pack_convt1d_weight(w.data_ptr<float>(), (int)cin, (int)cout, (int)stride,
+                                    (int)cout_pad, wp.data_ptr<float>(), stream_of(w)),
+           "vrvq_pack_convt1d_weight");
+  return wp;
+}
+
+// --------------------------------------------------------------------------- convs
+std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef shape,
+                                            const optional<Tensor>& alpha_out,
+                                            const optional<Tensor>& inv_alpha_out,
+                                            bool want_raw) {
+  TORCH_CHECK(alpha_out.has_value() == inv_alpha_out.has_value(),
+              "out_snake: alpha_out and inv_alpha_out go together");
+  if (alpha_out.has_value()) {
+    check_on(*alpha_out, like, "alpha_out");
+    check_on(*inv_alpha_out, like, "inv_alpha_out");
+    TORCH_CHECK(alpha_out->numel() == shape[1] && inv_alpha_out->numel() == shape[1],
+                "out_snake: one alpha per output channel");
+  }
+  Tensor ys = alpha_out.has_value() ? empty_f(shape, like) : none_like(like);
+  Tensor y = (want_raw || !alpha_out.has_value()) ? empty_f(shape, like) : none_like(like);
+  return {y, ys, Tensor()};
+}
+
+float* opt_ptr(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
+
+// Snake1d -> WNConv1d (+ residual, Tanh / Sigmoid, next Snake), models/layers.py:17-41, 52-89;
+// models/dac_vrvq.py:27-34, 62-74; models/importance_subnet.py:38-45.
+std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed, int64_t cout,
+                                        int64_t stride, int64_t pad, int64_t dil,
+                                        const optional<Tensor>& bias,
+                                        const optional<Tensor>& alpha,
+                                        const optional<Tensor>& inv_alpha,
+                                        const optional<Tensor>& residual, int64_t epilogue,
+                                        const optional<Tensor>& alpha_out,
+                                        const optional<Tensor>& inv_alpha_out, bool want_raw) {
+  check_t(x, "x");
+  check_on(w_packed, x, "w_packed");
+  check_opt(bias, x, "bias");
+  check_opt(alpha, x, "alpha");
+  check_opt(inv_alpha, x, "inv_alpha");
+  check_opt(residual, x, "residual");
+  TORCH_CHECK(x.dim() == 3, "conv1d: x must be (B, C, T)");
+  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1),
+              "conv1d: w_packed must be (Cin, k, cout_pad) with Cin = x.shape[1]");
+  TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(), "conv1d: snake needs inv_alpha");
+  c10::DeviceGuard guard(x.device());
+  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
+  const int64_t k = w_packed.size(1), cout_pad = w_packed.size(2);
+  const int64_t tout = (tin + 2 * pad - dil * (k - 1) - 1) / stride + 1;
+  TORCH_CHECK(tout > 0, "conv1d: input too short");
+  if (residual.has_value())
+    TORCH_CHECK(residual->sizes() == at::IntArrayRef({B, cout, tout}),
+                "conv1d: residual shape must equal the output shape");
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha), fp(inv_alpha),
+                       w_packed.data_ptr<float>(), (int)cout, (int)cout_pad, (int)k, (int)stride,
+                       (int)pad, (int)dil, fp(bias), fp(residual), (int)epilogue, opt_ptr(y),
+                       (int)tout, fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
+           "vrvq_conv1d");
+  return {y, ys};
+}
+
+// Snake1d -> WNConvTranspose1d (k = 2s) of DecoderBlock, models/layers.py:21-22, 92-103.
+std::tuple<Tensor, Tensor> snake_conv_transpose1d(
+    const Tensor& x, const Tensor& w_packed, int64_t cout, int64_t stride,
+    const optional<Tensor>& bias, const optional<Tensor>& alpha,
+    const optional<Tensor>& inv_alpha, const optional<Tensor>& alpha_out,
+    const optional<Tensor>& inv_alpha_out, bool want_raw) {
+  check_t(x, "x");
+  check_on(w_packed, x, "w_packed");
+  check_opt(bias, x, "bias");
+  check_opt(alpha, x, "alpha");
+  check_opt(inv_alpha, x, "inv_alpha");
+  TORCH_CHECK(x.dim() == 3, "conv_transpose1d: x must be (B, C, T)");
+  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1) && w_packed.size(1) == 2,
+              "conv_transpose1d: w_packed must be (Cin, 2, cout_pad)");
+  TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(),
+              "conv_transpose1d: snake needs inv_alpha");
+  c10::DeviceGuard guard(x.device());
+  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
+  const int64_t p = (stride + 1) / 2;
+  const int64_t tout = (tin - 1) * stride - 2 * p + 2 * stride;
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  check_rc(vrvq_conv_transpose1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                                 fp(inv_alpha), w_packed.data_ptr<float>(), (int)cout,
+                                 (int)w_packed.size(2), (int)stride, fp(bias), opt_ptr(y),
+                                 fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
+           "vrvq_conv_transpose1d");
+  return {y, ys};
+}
+
+// ResidualUnit in one launch, models/layers.py:52-68.
+std::tuple<Tensor, Tensor> residual_unit(const Tensor& x, const Tensor& x_snk, int64_t dil,
+                                         const Tensor& w7, const Tensor& b7,
+                                         const Tensor& alpha2, const Tensor& inv_alpha2,
+                                         const Tensor& w1, const Tensor& b1,
+                                         const optional<Tensor>& alpha_out,
+                                         const optional<Tensor>& inv_alpha_out, bool want_raw) {
+  check_t(x, "x");
+  check_on(x_snk, x, "x_snk");
+  check_on(w7, x, "w7");
+  check_on(b7, x, "b7");
+  check_on(alpha2, x, "alpha2");
+  check_on(inv_alpha2, x, "inv_alpha2");
+  check_on(w1, x, "w1");
+  check_on(b1, x, "b1");
+  TORCH_CHECK(x.dim() == 3 && x_snk.sizes() == x.sizes(),
+              "residual_unit: x_snk must have the shape of x (B, C, T)");
+  c10::DeviceGuard guard(x.device());
+  const int64_t B = x.size(0), C = x.size(1), T = x.size(2);
+  TORCH_CHECK(w7.dim() == 3 && w7.size(0) == C && w7.size(1) == 7 && w1.dim() == 3 &&
+                  w1.size(0) == C && w1.size(1) == 1 && w1.size(2) == w7.size(2),
+              "residual_unit: packed weights must be (C, 7, pad) and (C, 1, pad)");
+  auto [y, ys, _u] = out_pair(x, {B, C, T}, alpha_out, inv_alpha_out, want_raw);
+  check_rc(vrvq_residual_unit(x.data_ptr<float>(), x_snk.data_ptr<float>(), (int)B, (int)C,
+                              (int)T, (int)dil, w7.data_ptr<float>(), b7.data_ptr<float>(),
+                              alpha2.data_ptr<float>(), inv_alpha2.data_ptr<float>(),
+                              w1.data_ptr<float>(), b1.data_ptr<float>(), (int)w7.size(2),
+                              opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
+                              stream_of(x)),
+           "vrvq_residual_unit");
+  return {y, ys};
+}
+
+// --------------------------------------------------------------------------- RVQ
+void check_rvq_weights(const Tensor& z, const Tensor& w_in_t, const Tensor& b_in,
+                       const Tensor& cb, const Tensor& cbn, const Tensor& c2,
+                       const Tensor& w_out, const Tensor& b_out) {
+  check_on(w_in_t, z, "w_in_t");
+  check_on(b_in, z, "b_in");
+  check_on(cb, z, "cb");
+  check_on(cbn, z, "cbn");
+  check_on(c2, z, "c2");
+  check_on(w_out, z, "w_out");
+  check_on(b_out, z, "b_out");
+  TORCH_CHECK(cb.dim() == 3 && cbn.sizes() == cb.sizes(), "rvq: cb / cbn must be (nq, N, d)");
+  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2), D = z.size(1);
+  TORCH_CHECK(c2.numel() == nq * N, "rvq: c2 must be (nq, N)");
+  TORCH_CHECK(w_in_t.sizes() == at::IntArrayRef({nq, D, d}) &&
+                  w_out.sizes() == at::IntArrayRef({nq, D, d}),
+              "rvq: w_in_t / w_out must be (nq, D, d)");
+  TORCH_CHECK(b_in.numel() == nq * d && b_out.numel() == nq * D, "rvq: bias shapes");
+}
+
+// VBRResidualVectorQuantize.forward quantizer loop + gating (models/quantize.py:328-443) and
+// ResidualVectorQuantize.forward in eval (:136-214): all stages, z_q_is, mask, masked z_q.
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode(
+    const Tensor& z, const Tensor& w_in_t, const Tensor& b_in, const Tensor& cb,
+    const Tensor& cbn, const Tensor& c2, const Tensor& w_out, const Tensor& b_out,
+    const optional<Tensor>& imp, double level, bool want_z_q_is, bool want_mask) {
+  check_t(z, "z");
+  TORCH_CHECK(z.dim() == 3, "rvq_encode: z must be (B, D, T)");
+  check_rvq_weights(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out);
+  check_opt(imp, z, "imp");
+  c10::DeviceGuard guard(z.device());
+  const int64_t B = z.size(0), D = z.size(1), T = z.size(2);
+  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2);
+  if (imp.has_value()) TORCH_CHECK(imp->numel() == B * T, "rvq_encode: imp must hold B*T values");
+  Tensor codes = at::empty({B, nq, T}, z.options().dtype(at::kLong));
+  Tensor latents = empty_f({B, nq * d, T}, z);
+  Tensor loss_pf = empty_f({B, nq, T}, z);
+  Tensor z_q_is = want_z_q_is ? empty_f({B, nq, D, T}, z) : none_like(z);
+  Tensor z_q = empty_f({B, D, T}, z);
+  Tensor mask = want_mask ? empty_f({B, nq, T}, z) : none_like(z);
+  check_rc(vrvq_rvq_fused(z.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)N, (int)d,
+                          w_in_t.data_ptr<float>(), b_in.data_ptr<float>(), cb.data_ptr<float>(),
+                          cbn.data_ptr<float>(), c2.data_ptr<float>(), w_out.data_ptr<float>(),
+                          b_out.data_ptr<float>(), fp(imp), (float)level,
+                          codes.data_ptr<int64_t>(), latents.data_ptr<float>(),
+                          loss_pf.data_ptr<float>(), opt_ptr(z_q_is), z_q.data_ptr<float>(),
+                          opt_ptr(mask), stream_of(z)),
+           "vrvq_rvq_fused");
+  return {codes, latents, loss_pf, z_q_is, z_q, mask};
+}
+
+// decode_code of every stage (models/quantize.py:81-85) for from_codes (:217-249).
+// err is a 1-element int32 device tensor: 1 if a code was outside [0, N) (no host sync here;
+// the Python wrapper raises IndexError like F.embedding when it is allowed to synchronise).
+std::tuple<Tensor, Tensor, Tensor> rvq_gather(const Tensor& codes, const Tensor& cb) {
+  check_t(codes, "codes", at::kLong);
+  check_on(cb, codes, "cb");
+  TORCH_CHECK(codes.dim() == 3, "rvq_gather: codes must be (B, n_codebooks, T)");
+  TORCH_CHECK(cb.dim() == 3, "rvq_gather: cb must be (nq, N, d)");
+  c10::DeviceGuard guard(codes.device());
+  const int64_t B = codes.size(0), nq = codes.size(1), T = codes.size(2);
+  TORCH_CHECK(nq <= cb.size(0), "rvq_gather: ", nq, " codebooks requested, ", cb.size(0),
+              " available");
+  const int64_t N = cb.size(1), d = cb.size(2);
+  Tensor zst = empty_f({B, nq, T, d}, cb);
+  Tensor z_p = empty_f({B, nq * d, T}, cb);
+  Tensor err = at::zeros({1}, codes.options().dtype(at::kInt));
+  check_rc(vrvq_rvq_gather(codes.data_ptr<int64_t>(), (int)B, (int)nq, (int)T,
+                           cb.data_ptr<float>(), (int)N, (int)d, zst.data_ptr<float>(),
+                           z_p.data_ptr<float>(), err.data_ptr<int>(), stream_of(codes)),
+           "vrvq_rvq_gather");
+  return {zst, z_p, err};
+}
+
+// out_proj of every stage from straight-through / codebook rows + (masked) sum
+// (models/quantize.py:77, 217-249; scripts/inference.py:99-100).
+std::tuple<Tensor, Tensor, Tensor> rvq_expand(const Tensor& zst, const Tensor& w_out,
+                                              const Tensor& b_out, const optional<Tensor>& imp,
+                                              double level, bool want_z_q_is, bool want_mask) {
+  check_t(zst, "zst");
+  check_on(w_out, zst, "w_out");
+  check_on(b_out, zst, "b_out");
+  check_opt(imp, zst, "imp");
+  TORCH_CHECK(zst.dim() == 4, "rvq_expand: zst must be (B, nq, T, d)");
+  c10::DeviceGuard guard(zst.device());
+  const int64_t B = zst.size(0), nq = zst.size(1), T = zst.size(2), d = zst.size(3);
+  TORCH_CHECK(w_out.dim() == 3 && w_out.size(0) >= nq && w_out.size(2) == d,
+              "rvq_expand: w_out must be (>= nq, D, d)");
+  const int64_t D = w_out.size(1);
+  Tensor z_q_is = want_z_q_is ? empty_f({B, nq, D, T}, zst) : none_like(zst);
+  Tensor z_q = empty_f({B, D, T}, zst);
+  Tensor mask = want_mask ? empty_f({B, nq, T}, zst) : none_like(zst);
+  check_rc(vrvq_rvq_expand(zst.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)d,
+                           w_out.data_ptr<float>(), b_out.data_ptr<float>(), fp(imp),
+                           (float)level, opt_ptr(z_q_is), z_q.data_ptr<float>(), opt_ptr(mask),
+                           stream_of(zst)),
+           "vrvq_rvq_expand");
+  return {z_q_is, z_q, mask};
+}
+
+// (loss * mask).sum(1).mean(), models/quantize.py:422-423.
+Tensor masked_loss(const Tensor& loss_pf, const optional<Tensor>& mask) {
+  check_t(loss_pf, "loss_pf");
+  check_opt(mask, loss_pf, "mask");
+  TORCH_CHECK(loss_pf.dim() == 3, "masked_loss: loss_pf must be (B, nq, T)");
+  c10::DeviceGuard guard(loss_pf.device());
+  Tensor out = empty_f({}, loss_pf);
+  check_rc(vrvq_masked_loss(loss_pf.data_ptr<float>(), fp(mask), (int)loss_pf.size(0),
+                            (int)loss_pf.size(1), (int)loss_pf.size(2), out.data_ptr<float>(),
+                            stream_of(loss_pf)),
+           "vrvq_masked_loss");
+  return out;
+}
+
+// imp_map * a * c (models/quantize.py:389, scripts/inference.py:96-97).
+Tensor scale_imp(const Tensor& imp, double a, double c) {
+  check_t(imp, "imp");
+  c10::DeviceGuard guard(imp.device());
+  Tensor s = at::empty_like(imp);
+  check_rc(vrvq_scale_imp(imp.data_ptr<float>(), (int)imp.numel(), (float)a, (float)c,
+                          s.data_ptr<float>(), stream_of(imp)),
+           "vrvq_scale_imp");
+  return s;
+}
+
+// generate_mask_hard, models/utils.py:55-61: s (B, 1, T) -> mask (B, nq, T).
+Tensor imp_mask(const Tensor& s, int64_t nq) {
+  check_t(s, "x");
+  TORCH_CHECK(s.dim() >= 2, "generate_mask_hard: x must be (B, 1, T)");
+  const int64_t B = s.size(0), T = s.size(-1);
+  TORCH_CHECK(s.numel() == B * T, "generate_mask_hard: x must be (B, 1, T)");
+  c10::DeviceGuard guard(s.device());
+  Tensor mask = empty_f({B, nq, T}, s);
+  check_rc(vrvq_mask_hard(s.data_ptr<float>(), (int)B, (int)T, (int)nq, mask.data_ptr<float>(),
+                          stream_of(s)),
+           "vrvq_mask_hard");
+  return mask;
+}
+
+// sum_i z_q_is[:, i] * mask[:, i, None, :], scripts/inference.py:99-100.
+Tensor masked_sum(const Tensor& z_q_is, const Tensor& mask) {
+  check_t(z_q_is, "z_q_is");
+  check_on(mask, z_q_is, "mask");
+  TORCH_CHECK(z_q_is.dim() == 4, "masked_sum: z_q_is must be (B, nq, D, T)");
+  const int64_t B = z_q_is.size(0), nq = z_q_is.size(1), D = z_q_is.size(2), T = z_q_is.size(3);
+  TORCH_CHECK(mask.sizes() == at::IntArrayRef({B, nq, T}), "masked_sum: mask must be (B, nq, T)");
+  c10::DeviceGuard guard(z_q_is.device());
+  Tensor z_q = empty_f({B, D, T}, z_q_is);
+  check_rc(vrvq_masked_sum(z_q_is.data_ptr<float>(), mask.data_ptr<float>(), (int)B, (int)nq,
+                           (int)D, (int)T, z_q.data_ptr<float>(), stream_of(z_q_is)),
+           "vrvq_masked_sum");
+  return z_q;
+}
+
+// cal_bpf_from_mask, models/utils.py:64-73 (0-d device tensor, no host sync).
+Tensor bpf(const Tensor& mask, const Tensor& bits) {
+  check_t(mask, "mask");
+  check_on(bits, mask, "bits");
+  TORCH_CHECK(mask.dim() == 3, "cal_bpf_from_mask: mask must be (B, nq, T)");
+  TORCH_CHECK(bits.numel() == mask.size(1), "cal_bpf_from_mask: one bit count per codebook");
+  c10::DeviceGuard guard(mask.device());
+  Tensor out = empty_f({}, mask);
+  check_rc(vrvq_bpf(mask.data_ptr<float>(), bits.data_ptr<float>(), (int)mask.size(0),
+                    (int)mask.size(1), (int)mask.size(2), out.data_ptr<float>(), stream_of(mask)),
+           "vrvq_bpf");
+  return out;
+}
+
+// --------------------------------------------------------------------------- code packing
+// Variable-length packing. The packed length is data-dependent, so
+// pack_codes takes it from the host (vrvq_amd/codes_io.py reads clip_off[B]).
+std::tuple<Tensor, Tensor, Tensor> pack_counts(const Tensor& mask) {
+  check_t(mask, "mask");
+  TORCH_CHECK(mask.dim() == 3, "pack_counts: mask must be (B, Nq, T)");
+  c10::DeviceGuard guard(mask.device());
+  const int64_t B = mask.size(0), nq = mask.size(1), T = mask.size(2);
+  Tensor counts = at::empty({B, T}, mask.options().dtype(at::kInt));
+  Tensor tot = at::empty({B}, mask.options().dtype(at::kLong));
+  Tensor off = at::empty({B + 1}, mask.options().dtype(at::kLong));
+  Tensor err = at::zeros({1}, mask.options().dtype(at::kInt));
+  check_rc(vrvq_pack_counts(mask.data_ptr<float>(), (int)B, (int)nq, (int)T,
+                            counts.data_ptr<int>(),
+                            reinterpret_cast<long long*>(tot.data_ptr<int64_t>()),
+                            reinterpret_cast<long long*>(off.data_ptr<int64_t>()),
+                            err.data_ptr<int>(), stream_of(mask)),
+           "vrvq_pack_counts");
+  return {counts, off, err};
+}
+
+std::tuple<Tensor, Tensor> pack_codes(const Tensor& codes, const Tensor& counts,
+                                      const Tensor& clip_off, int64_t total, int64_t ncode) {
+  check_t(codes, "codes", at::kLong);
+  check_on(counts, codes, "counts", at::kInt);
+  check_on(clip_off, codes, "clip_off", at::kLong);
+  TORCH_CHECK(codes.dim() == 3, "pack_codes: codes must be (B, Nq, T)");
+  c10::DeviceGuard guard(codes.device());
+  const int64_t B = codes.size(0), nq = codes.size(1), T = codes.size(2);
+  Tensor packed = at::empty({total}, codes.options().dtype(at::kShort));
+  Tensor err = at::zeros({1}, codes.options().dtype(at::kInt));
+  if (total > 0)
+    check_rc(vrvq_pack_codes(codes.data_ptr<int64_t>(), counts.data_ptr<int>(),
+                             reinterpret_cast<const long long*>(clip_off.data_ptr<int64_t>()),
+                             (int)B, (int)nq, (int)T, (int)ncode,
+                             reinterpret_cast<uint16_t*>(packed.data_ptr<int16_t>()),
+                             err.data_ptr<int>(), stream_of(codes)),
+             "vrvq_pack_codes");
+  return {packed, err};
+}
+
+Tensor unpack_offsets(const Tensor& counts) {
+  check_t(counts, "counts", at::kInt);
+  TORCH_CHECK(counts.dim() == 2, "unpack: counts must be (B, T)");
+  c10::DeviceGuard guard(counts.device());
+  const int64_t B = counts.size(0), T = counts.size(1);
+  Tensor tot = at::empty({B}, counts.options().dtype(at::kLong));
+  Tensor off = at::empty({B + 1}, counts.options().dtype(at::kLong));
+  check_rc(vrvq_unpack_offsets(counts.data_ptr<int>(), (int)B, (int)T,
+                               reinterpret_cast<long long*>(tot.data_ptr<int64_t>()),
+                               reinterpret_cast<long long*>(off.data_ptr<int64_t>()),
+                               stream_of(counts)),
+           "vrvq_unpack_offsets");
+  return off;
+}
+
+std::tuple<Tensor, Tensor> unpack_codes(const Tensor& packed, const Tensor& counts,
+                                        const Tensor& clip_off, int64_t n_codebooks) {
+  check_t(counts, "counts", at::kInt);
+  check_on(packed, counts, "packed", at::kShort);
+  check_on(clip_off, counts, "clip_off", at::kLong);
+  TORCH_CHECK(counts.dim() == 2 && packed.dim() == 1, "unpack: counts (B, T), packed 1-D");
+  TORCH_CHECK(n_codebooks > 0 && n_codebooks <= 255, "unpack: n_codebooks in [1, 255]");
+  c10::DeviceGuard guard(counts.device());
+  const int64_t B = counts.size(0), T = counts.size(1);
+  Tensor codes = at::empty({B, n_codebooks, T}, counts.options().dtype(at::kLong));
+  Tensor mask = empty_f({B, n_codebooks, T}, counts);
+  Tensor src = packed.numel() ? packed : at::zeros({1}, packed.options());
+  check_rc(vrvq_unpack_codes(reinterpret_cast<const uint16_t*>(src.data_ptr<int16_t>()),
+                             counts.data_ptr<int>(),
+                             reinterpret_cast<const long long*>(clip_off.data_ptr<int64_t>()),
+                             (int)B, (int)n_codebooks, (int)T, codes.data_ptr<int64_t>(),
+                             mask.data_ptr<float>(), stream_of(counts)),
+           "vrvq_unpack_codes");
+  return {codes, mask};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(vrvq, m) {
+  m.def("weight_norm(Tensor g, Tensor v) -> Tensor");
+  m.def("snake_inv_alpha(Tensor alpha) -> Tensor");
+  m.def("codebook_prep(Tensor cb) -> (Tensor, Tensor)");
+  m.def("pack_conv1d_weight(Tensor w) -> Tensor");
+  m.def("pack_convt1d_weight(Tensor w, int stride) -> Tensor");
+  m.def(
+      "snake_conv1d(Tensor x, Tensor w_packed, int cout, int stride, int pad, int dil, "
+      "Tensor? bias, Tensor? alpha, Tensor? inv_alpha, Tensor? residual, int epilogue, "
+      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw) -> (Tensor, Tensor)");
+  m.def(
+      "snake_conv_transpose1d(Tensor x, Tensor w_packed, int cout, int stride, Tensor? bias, "
+      "Tensor? alpha, Tensor? inv_alpha, Tensor? alpha_out, Tensor? inv_alpha_out, "
+      "bool want_raw) -> (Tensor, Tensor)");
+  m.def(
+      "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
+      "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "
+      "bool want_raw) -> (Tensor, Tensor)");
+  m.def(
+      "rvq_encode(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbn, Tensor c2, "
+      "Tensor w_out, Tensor b_out, Tensor? imp, float level, bool want_z_q_is, bool want_mask) "
+      "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("rvq_gather(Tensor codes, Tensor cb) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "rvq_expand(Tensor zst, Tensor w_out, Tensor b_out, Tensor? imp, float level, "
+      "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor)");
+  m.def("masked_loss(Tensor loss_pf, Tensor? mask) -> Tensor");
+  m.def("scale_imp(Tensor imp, float a, float c) -> Tensor");
+  m.def("imp_mask(Tensor s, int nq) -> Tensor");
+  m.def("masked_sum(Tensor z_q_is, Tensor mask) -> Tensor");
+  m.def("bpf(Tensor mask, Tensor bits) -> Tensor");
+  m.def("pack_counts(Tensor mask) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "pack_codes(Tensor codes, Tensor counts, Tensor clip_off, int total, int ncode) "
+      "-> (Tensor, Tensor)");
+  m.def("unpack_offsets(Tensor counts) -> Tensor");
+  m.def(
+      "unpack_codes(Tensor packed, Tensor counts, Tensor clip_off, int n_codebooks) "
+      "-> (Tensor, Tensor)");
+}
+
+#define VRVQ_IMPLS(m) \
+  m.impl("weight_norm", &weight_norm); \
+  m.impl("snake_inv_alpha", &snake_inv_alpha); \
+  m.impl("codebook_prep", &codebook_prep); \
+  m.impl("pack_conv1d_weight", &pack_conv1d_weight); \
+  m.impl("pack_convt1d_weight", &pack_convt1d_weight); \
+  m.impl("snake_conv1d", &snake_conv1d); \
+  m.impl("snake_conv_transpose1d", &snake_conv_transpose1d); \
+  m.impl("residual_unit", &residual_unit); \
+  m.impl("rvq_encode", &rvq_encode); \
+  m.impl("rvq_gather", &rvq_gather); \
+  m.impl("rvq_expand", &rvq_expand); \
+  m.impl("masked_loss", &masked_loss); \
+  m.impl("scale_imp", &scale_imp); \
+  m.impl("imp_mask", &imp_mask); \
+  m.impl("masked_sum", &masked_sum); \
+  m.impl("bpf", &bpf); \
+  m.impl("pack_counts", &pack_counts); \
+  m.impl("pack_codes", &pack_codes); \
+  m.impl("unpack_offsets", &unpack_offsets); \
+  m.impl("unpack_codes", &unpack_codes); \
+
+TORCH_LIBRARY_IMPL(vrvq, CUDA, m) { VRVQ_IMPLS(m) }
+
+// CPU tensors reach the same functions, whose first TORCH_CHECK raises "vrvq kernels run on the
+// GPU only": there is no CPU fallback, and the error says so instead of a dispatcher miss.
+TORCH_LIBRARY_IMPL(vrvq, CPU, m) { VRVQ_IMPLS(m) }

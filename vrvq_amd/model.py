@@ -115,7 +115,7 @@ class VectorQuantize(nn.Module):
         Returns z_q, commitment_loss, codebook_loss, indices, z_e as the reference does
         (losses per frame (B, T) if loss_per_frame else per item (B,))."""
         st = _stack_stages([self], z.device)
-        codes, latents, loss_pf, _, z_q, _ = ops.rvq_fused(
+        codes, latents, loss_pf, _, z_q, _ = ops.rvq_encode(
             z.contiguous(), *st.codes_args(), want_z_q_is=False, want_mask=False)
         loss = loss_pf[:, 0, :]
         if not loss_per_frame:
@@ -142,17 +142,14 @@ class _Stacked:
         self.cbn, self.c2 = ops.codebook_prep(self.cb)
         self.w_out = torch.stack(w_out).contiguous()
         self.b_out = torch.stack(b_out).contiguous()
-        # cross terms of the projected chain (include/vrvq.h, vrvq_rvq_cross_prep)
-        self.mcol, self.qb = ops.rvq_cross_prep(self.w_in_t, self.w_out, self.b_out)
 
     def codes_args(self):
         return (self.w_in_t, self.b_in, self.cb, self.cbn, self.c2, self.w_out, self.b_out)
 
     def prefix(self, n):
         s = _Stacked.__new__(_Stacked)
-        for k in ("w_in_t", "b_in", "cb", "cbn", "c2", "w_out", "b_out", "qb"):
+        for k in ("w_in_t", "b_in", "cb", "cbn", "c2", "w_out", "b_out"):
             setattr(s, k, getattr(self, k)[:n].contiguous())
-        s.mcol = self.mcol[:n, :n].contiguous()
         return s
 
 
@@ -200,7 +197,7 @@ class ResidualVectorQuantize(nn.Module):
         st = self.stacked()
         if n < self.n_codebooks:
             st = st.prefix(n)
-        codes, latents, loss_pf, _, z_q, _ = ops.rvq_fused(
+        codes, latents, loss_pf, _, z_q, _ = ops.rvq_encode(
             z.contiguous(), *st.codes_args(), want_z_q_is=False, want_mask=False)
         loss = ops.masked_loss(loss_pf, None)  # sum_i mean_{b,t} loss_i (mask all-true in eval)
         return {"z_q": z_q, "codes": codes, "latents": latents,
@@ -278,9 +275,8 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
             imp, lvl = imp_map.reshape(B, T), float(level)
         else:
             imp_map, imp, lvl = None, None, 1.0
-        # one launch: residual chain, z_q_is stream, importance mask, masked z_q
-        # (ops.rvq_encode is the three-launch projected-chain alternative, same outputs)
-        codes, latents, loss_pf, z_q_is, z_q, mask = ops.rvq_fused(
+        # residual chain, z_q_is stream, importance mask, masked z_q
+        codes, latents, loss_pf, z_q_is, z_q, mask = ops.rvq_encode(
             z.contiguous(), *st.codes_args(), imp=imp, level=lvl, want_z_q_is=want_z_q_is)
         loss = ops.masked_loss(loss_pf, mask)
         return {
