@@ -39,10 +39,6 @@ enum vrvq_epilogue_t { VRVQ_EPI_NONE = 0, VRVQ_EPI_TANH = 1, VRVQ_EPI_SIGMOID = 
 const char* vrvq_status_string(int status);
 /* Library version (major*10000 + minor*100 + patch). */
 int vrvq_version(void);
-/* Diagnostics: in a library built with -DVRVQ_STAMPS, vrvq_rvq_codes writes per-workgroup,
- * per-stage s_memtime stamps ([blocks][nq][8] uint64) into buf (NULL disables). A no-op in
- * the product build. */
-int vrvq_debug_set_stamps(unsigned long long* buf);
 
 /* ---------------------------------------------------------------------------------------
  * Weight preparation (once per load_state_dict; the reference recomputes weight norm on
@@ -132,10 +128,8 @@ int vrvq_pack_convt1d_weight(const float* w, int cin, int cout, int stride, int 
 
 /* ---------------------------------------------------------------------------------------
  * Residual vector quantisation (VBRResidualVectorQuantize.forward, models/quantize.py:328-443;
- * per stage VectorQuantize.forward/decode_latents, models/quantize.py:42-103).
- *
- * Stage 1 (vrvq_rvq_codes): the sequential residual chain, all nq stages in one launch.
- * Per frame (b,t) and stage i:
+ * per stage VectorQuantize.forward/decode_latents, models/quantize.py:42-103). Per frame (b,t)
+ * and stage i:
  *   z_e   = W_in[i] r + b_in[i]                    (in_proj, WN k=1 conv D->d)
  *   e     = z_e / max(||z_e||, 1e-12)
  *   idx   = argmin_n ( (sum e^2 - 2 e.cbn[i,n]) + c2[i,n] ), lowest n on ties
@@ -143,75 +137,78 @@ int vrvq_pack_convt1d_weight(const float* w, int cin, int cout, int stride, int 
  *   loss  = mean_k (z_e - zq)^2                    (commitment == codebook loss in forward)
  *   zst   = z_e + (zq - z_e)                       (straight-through value)
  *   r    -= W_out[i] zst + b_out[i]                (out_proj, WN k=1 conv d->D)
+ * By linearity of in_proj / out_proj,
+ *   z_e(i) = ((P_i + b_in[i]) - Qb_i) - sum_{j<i} M_ij zst_j,
+ *   P_i = W_in[i] z,  M_ij = W_in[i] W_out[j] (8x8),  Qb_i = W_in[i] sum_{j<i} b_out[j],
+ * so the sequential chain runs in the 8-dim latent space (vrvq_rvq_chain) between two
+ * parallel 1024-dim passes: the projection of z for every stage (vrvq_rvq_project) and the
+ * expansion of z_q_is / z_q with the reference's out_proj expression (vrvq_rvq_expand).
  *
  *   z       [B][D][T]         encoder output
  *   w_in_t  [nq][D][d]        folded in_proj weight, transposed (d fastest)
  *   b_in    [nq][d]
- *   cb, cbn [nq][N][d]        raw / normalised codebooks; c2 [nq][N]
+ *   cb      [nq][N][d]        raw codebooks; c2 [nq][N] squared norms of the normalised rows
+ *   cbf     [nq][8][64][N/128][2]  normalised codebooks in the chain's MFMA fragment order
+ *                             (vrvq_rvq_frag of vrvq_codebook_prep's cbn)
  *   w_out   [nq][D][d]        folded out_proj weight; b_out [nq][D]
+ *   imp     [B][T] importance map, or NULL (CBR: mask = 1, models/quantize.py:397-400)
+ *   level   s[b,t] = (imp[b,t] * level) * nq, mask[b,i,t] = (s - i >= 0)   (models/quantize.py:389,
+ *           models/utils.py:45-61)
  * outputs:
  *   codes   [B][nq][T] int64  (torch argmax indices)
  *   latents [B][nq*d][T]      concatenated z_e
  *   loss_pf [B][nq][T]        per-frame loss
- *   zst     [B][nq][T][d]     straight-through codebook vectors (input of stage 2)
- * Supported: D == 1024 (latent_dim of every shipped config), d == 8, N % 256 == 0.
+ *   z_q_is  [B][nq][D][T]     per-stage out_proj values (or NULL: not materialised)
+ *   z_q     [B][D][T]         sum_i mask[b,i,t] * z_q_is[b,i,:,t], stage order
+ *   mask    [B][nq][T]        (or NULL)
+ * Supported: D == 1024 (latent_dim of every shipped config), d == 8, nq <= 32,
+ * N % 256 == 0 and N <= 1024.
  * ------------------------------------------------------------------------------------- */
-int vrvq_rvq_codes(const float* z, int batch, int dim, int frames, int nq, int ncode,
-                   int cdim, const float* w_in_t, const float* b_in, const float* cb,
-                   const float* cbn, const float* c2, const float* w_out, const float* b_out,
-                   int64_t* codes, float* latents, float* loss_pf, float* zst,
-                   vrvq_stream_t stream);
-
-/* Projected chain (the production RVQ path: vrvq_rvq_project -> vrvq_rvq_chain ->
- * vrvq_rvq_expand). By linearity of in_proj / out_proj, stage i's projection of the residual
- * (models/quantize.py:353-365) is
- *   z_e(i) = ((P_i + b_in[i]) - Qb_i) - sum_{j<i} M_ij zst_j,
- *   P_i = W_in[i] z,  M_ij = W_in[i] W_out[j] (8x8),  Qb_i = W_in[i] sum_{j<i} b_out[j],
- * so the chain runs in the 8-dim latent space; z_q_is / z_q come from vrvq_rvq_expand with the
- * reference's own out_proj expression. */
 
 /* Once per weight version: mcol [nq][nq][d][d] with mcol[j][i] = M_ij for i > j (else 0) and
- * qb [nq][d]. Supported: D == 1024, d == 8. */
+ * qb [nq][d]. */
 int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_out, int nq,
                         int dim, int cdim, float* mcol, float* qb, vrvq_stream_t stream);
 
-/* P partial sums over 8 channel splits: part [8][B*T][nq*d], part[s][b*T+t][i*d+k] =
+/* Once per weight version: cbf[i][w][l][t][h] = cbn[i][w*N/8 + 16t + (l&15)][4h + (l>>4)]. */
+int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
+                  vrvq_stream_t stream);
+
+/* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows). */
+int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
+
+/* The whole quantizer in three stream-ordered launches (project -> chain -> expand), the
+ * replacement of VBRResidualVectorQuantize.forward's quantizer loop, importance mask and masked
+ * sum (models/quantize.py:353-365, 389-421) and of ResidualVectorQuantize.forward in eval
+ * (:136-214). workspace: >= vrvq_rvq_workspace() bytes, 16-byte aligned, caller-owned, no
+ * initialisation needed. */
+int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
+                    const float* w_in_t, const float* b_in, const float* cb, const float* cbf,
+                    const float* c2, const float* w_out, const float* b_out, const float* mcol,
+                    const float* qb, const float* imp, float level, int64_t* codes,
+                    float* latents, float* loss_pf, float* z_q_is, float* z_q, float* mask,
+                    void* workspace, long long workspace_bytes, vrvq_stream_t stream);
+
+/* Step 1: P partial sums over 8 channel splits: part [8][B*T][nq*d], part[s][b*T+t][i*d+k] =
  * sum_{c in split s} W_in[i][k][c] z[b][c][t] (in_proj without bias, all stages at once). */
 int vrvq_rvq_project(const float* z, int batch, int dim, int frames, int nq, int cdim,
                      const float* w_in_t, float* part, vrvq_stream_t stream);
 
-/* The 8-dim chain over all nq stages (P = sum of the 8 partials in split order). Outputs as
- * vrvq_rvq_codes (codes, latents = z_e, loss_pf, zst) plus mask [B][nq][T] (or NULL) from
- * imp / level as in vrvq_rvq_expand. Supported: d == 8, nq <= 32, N % 256 == 0, N <= 1024. */
+/* Step 2: the 8-dim chain over all nq stages (P = sum of the 8 partials in split order).
+ * Outputs codes, latents (= z_e), loss_pf, zst [B][nq][T][d] (straight-through rows, the input
+ * of step 3) and mask (or NULL). */
 int vrvq_rvq_chain(const float* part, int batch, int frames, int nq, int ncode, int cdim,
                    const float* b_in, const float* qb, const float* mcol, const float* cb,
-                   const float* cbn, const float* c2, const float* imp, float level,
+                   const float* cbf, const float* c2, const float* imp, float level,
                    int64_t* codes, float* latents, float* loss_pf, float* zst, float* mask,
                    vrvq_stream_t stream);
 
-/* Single launch (vrvq_rvq_fused): stage 1 + stage 2 in one kernel — the residual chain above,
- * plus, per stage, z_q_is[b,i,:,t] (the chain's own out_proj value, streamed to HBM as it is
- * produced), the importance mask and the masked sum z_q of vrvq_rvq_expand below. Outputs are
- * bit-identical to vrvq_rvq_codes + vrvq_rvq_expand except for the in_proj partial-sum order.
- * Replaces VBRResidualVectorQuantize.forward's quantizer loop and masking
- * (models/quantize.py:353-365, 389-421) and ResidualVectorQuantize.forward (:136-214, eval).
- *   imp     [B][T] importance map or NULL (CBR: mask = 1); level as in vrvq_rvq_expand
- *   z_q_is  [B][nq][D][T] or NULL (not materialised); mask [B][nq][T] or NULL
- *   codes, latents, loss_pf as in vrvq_rvq_codes; z_q [B][D][T]
- * Supported: D == 1024, d == 8, N % 256 == 0 and N <= 1024, D*T < 2^32. */
-int vrvq_rvq_fused(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
-                   const float* w_in_t, const float* b_in, const float* cb, const float* cbn,
-                   const float* c2, const float* w_out, const float* b_out, const float* imp,
-                   float level, int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
-                   float* z_q, float* mask, vrvq_stream_t stream);
-
-/* Stage 2 (vrvq_rvq_expand): HBM-streaming expansion + importance gating.
- *   z_q_is[b,i,:,t] = W_out[i] zst[b,i,t] + b_out[i]          (bit-identical to stage 1)
- *   s[b,t]          = (imp[b,t] * level) * nq                 (models/quantize.py:389)
- *   mask[b,i,t]     = s[b,t] - i >= 0 ? 1 : 0                 (models/utils.py:45-61)
+/* Step 3: HBM-streaming expansion + importance gating.
+ *   z_q_is[b,i,:,t] = W_out[i] zst[b,i,t] + b_out[i]          (models/quantize.py:77)
  *   z_q[b,:,t]      = sum_i mask[b,i,t] * z_q_is[b,i,:,t]     (models/quantize.py:420-421)
- * imp == NULL selects the reference's CBR branch (mask = 1, models/quantize.py:397-400).
- * z_q_is may be NULL (not materialised). mask may be NULL. */
+ * imp == NULL: mask = 1 (CBR, and from_codes). z_q_is may be NULL (not materialised); mask, if
+ * not NULL, receives the mask. Also the second half of from_codes (models/quantize.py:217-249)
+ * after vrvq_rvq_gather. */
 int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames, int nq, int cdim,
                     const float* w_out, const float* b_out, const float* imp, float level,
                     float* z_q_is, float* z_q, float* mask, vrvq_stream_t stream);

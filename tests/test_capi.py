@@ -25,7 +25,7 @@ def header_functions():
 
 def test_header_parsed():
     decls = header_functions()
-    assert "vrvq_rvq_codes" in decls and "vrvq_conv1d" in decls and len(decls) >= 16
+    assert "vrvq_rvq_encode" in decls and "vrvq_conv1d" in decls and len(decls) >= 16
 
 
 def test_library_exports_every_declared_symbol():
@@ -58,7 +58,11 @@ def test_argument_errors_raise_before_launch():
     assert lib.vrvq_weight_norm(None, None, 4, 4, None, None) == 10001
     assert lib.vrvq_conv1d(None, 1, 1, 8, None, None, None, 1, 128, 3, 1, 1, 1, None, None, 0,
                            None, 8, None, None, None, None) == 10001
-    assert lib.vrvq_rvq_codes(*([None] + [1] * 6 + [None] * 12)) == 10001
+    assert lib.vrvq_rvq_encode(*([None] + [1] * 6 + [None] * 10 + [1.0] + [None] * 7 +
+                                 [0, None])) == 10001
+    n = ctypes.c_longlong(0)
+    assert lib.vrvq_rvq_workspace(32, 87, 8, ctypes.byref(n)) == 0
+    assert n.value == (8 * 32 * 87 * 64 + 32 * 87 * 8 * 8) * 4
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
     # geometry mismatch (tout inconsistent with the conv formula)

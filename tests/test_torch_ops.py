@@ -12,7 +12,7 @@ from vrvq_amd import ops
 
 EXPECTED = ["weight_norm", "snake_inv_alpha", "codebook_prep", "pack_conv1d_weight",
             "pack_convt1d_weight", "snake_conv1d", "snake_conv_transpose1d", "residual_unit",
-            "rvq_encode", "rvq_gather", "rvq_expand", "masked_loss", "scale_imp", "imp_mask",
+            "rvq_cross_prep", "rvq_frag", "rvq_encode", "rvq_gather", "rvq_expand", "masked_loss", "scale_imp", "imp_mask",
             "masked_sum", "bpf", "pack_counts", "pack_codes", "unpack_offsets", "unpack_codes"]
 
 
@@ -44,9 +44,11 @@ def test_fake_kernels_propagate_shapes():
     z = torch.empty(3, 1024, 87, device=m)
     cb = torch.empty(8, 1024, 8, device=m)
     w = torch.empty(8, 1024, 8, device=m)
+    mcol, qb = vr.rvq_cross_prep(w, w, torch.empty(8, 1024, device=m))
+    assert mcol.shape == (8, 8, 8, 8) and qb.shape == (8, 8)
     out = vr.rvq_encode(z, w, torch.empty(8, 8, device=m), cb, cb, torch.empty(8, 1024, device=m),
-                        w, torch.empty(8, 1024, device=m), torch.empty(3, 87, device=m), 1.0,
-                        True, True)
+                        w, torch.empty(8, 1024, device=m), mcol, qb, torch.empty(3, 87, device=m),
+                        1.0, True, True)
     assert [tuple(o.shape) for o in out] == [(3, 8, 87), (3, 64, 87), (3, 8, 87),
                                              (3, 8, 1024, 87), (3, 1024, 87), (3, 8, 87)]
     assert out[0].dtype == torch.int64

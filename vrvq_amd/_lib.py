@@ -29,14 +29,15 @@ SIGNATURES = {
                            _P],
     "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
-    "vrvq_rvq_codes": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
-    "vrvq_rvq_expand": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
     "vrvq_rvq_cross_prep": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "vrvq_rvq_frag": [_P, _I, _I, _I, _P, _P],
+    "vrvq_rvq_workspace": [_I, _I, _I, _P],
+    "vrvq_rvq_encode": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
+                        _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_rvq_project": [_P, _I, _I, _I, _I, _I, _P, _P, _P],
     "vrvq_rvq_chain": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P,
                        _P],
-    "vrvq_rvq_fused": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P,
-                       _P, _P, _P, _P],
+    "vrvq_rvq_expand": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
     "vrvq_rvq_gather": [_P, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P],
     "vrvq_masked_loss": [_P, _P, _I, _I, _I, _P, _P],
     "vrvq_mask_hard": [_P, _I, _I, _I, _P, _P],
@@ -48,8 +49,7 @@ SIGNATURES = {
     "vrvq_unpack_offsets": [_P, _I, _I, _P, _P, _P],
     "vrvq_unpack_codes": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
 }
-EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
-         "vrvq_debug_set_stamps": ([_P], _I)}
+EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)}
 
 _lock = threading.Lock()
 _lib = None

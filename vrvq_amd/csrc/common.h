@@ -16,9 +16,6 @@ static inline int vrvq_launch_status() {
   return e == hipSuccess ? 0 : (int)e;
 }
 
-// Diagnostic stamp buffer (vrvq_debug_set_stamps; written only by -DVRVQ_STAMPS builds).
-extern unsigned long long* vrvq_g_stamps;
-
 static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Snake activation, models/layers.py:30: x + (alpha + 1e-9)^-1 * sin(alpha * x)^2.
@@ -42,9 +39,8 @@ __device__ __forceinline__ float dot8(const float4& a0, const float4& a1, const 
   return acc;
 }
 
-// out_proj of one frame for one output channel: (W_out[c,:] . zst) + b_out[c].
-// Shared by vrvq_rvq_codes (residual update) and vrvq_rvq_expand (z_q_is), so both
-// produce the same bits.
+// out_proj of one frame for one output channel: (W_out[c,:] . zst) + b_out[c]
+// (vrvq_rvq_expand's z_q_is).
 __device__ __forceinline__ float out_proj1(const float4& w0, const float4& w1, float bias,
                                            const float4& z0, const float4& z1) {
   return dot8(w0, w1, z0, z1) + bias;

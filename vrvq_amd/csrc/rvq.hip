@@ -1,487 +1,762 @@
-// Residual vector quantisation for gfx950: VBRResidualVectorQuantize.forward
-// (models/quantize.py:328-443) split into two launches.
+// Residual vector quantisation on gfx950: projection GEMM -> 8-dim chain -> HBM expansion.
 //
-//  vrvq_rvq_codes  — the sequential residual chain (in_proj, L2-normalise, cosine-NN argmin
-//                    over the codebook, straight-through vector, out_proj, residual update)
-//                    for all nq stages in one launch. One workgroup owns F frames; each
-//                    thread owns D/256 latent channels x F frames of the residual in VGPRs,
-//                    so every weight / codebook value it loads is reused F times from a
-//                    register. Weights stream from L2 with coalesced float4 loads.
-//  vrvq_rvq_expand — pure HBM streaming: recomputes z_q_is = out_proj(zst) (bit-identical
-//                    expression to the chain's), applies the importance mask and writes
-//                    z_q_is / z_q / mask as contiguous float4 rows. This is where ~95 % of the
-//                    algorithmic bytes go (nq*D*4 B per frame).
+// VBRResidualVectorQuantize.forward (models/quantize.py:328-443) runs, per frame and stage i
+// (VectorQuantize.forward / decode_latents, :42-103):
+//   z_e(i) = W_in(i) r_i + b_in(i),     r_i = z - sum_{j<i} z_q_j,   z_q_j = W_out(j) zst_j + b_out(j)
+//   idx    = argmin_n (sum e^2 - 2 e.cbn_n) + sum cbn_n^2,  e = z_e / max(|z_e|, 1e-12)
+//   zst_i  = z_e + (cb[idx] - z_e)                               (straight-through value)
+// By linearity z_e(i) = ((P_i + b_in(i)) - Qb_i) - sum_{j<i} M_ij zst_j with P_i = W_in(i) z,
+// M_ij = W_in(i) W_out(j) (8x8) and Qb_i = W_in(i) sum_{j<i} b_out(j): the sequential part
+// lives in the 8-dim latent space and the 1024-dim work becomes two embarrassingly parallel
+// streams. Three launches:
+//
+//   rvq_project_kernel   P partials over 8 channel splits (v_mfma_f32_16x16x4_f32): each
+//                        workgroup streams one clip's 128-channel slab of z once (contiguous
+//                        rows, K chunks double-buffered in LDS under the MFMAs).
+//   rvq_chain_kernel     the chain: <= 16 frames per workgroup, 8 waves; wave w scans its
+//                        N/8 codes for all frames at once on the matrix cores (16-code x
+//                        16-frame MFMA tiles), then 8 (frame, k) lane groups finish the stage
+//                        (cross-wave argmin, raw codeword, loss, projected residual, next z_e)
+//                        — two barriers per stage, no global stores until the end.
+//   rvq_expand_kernel    z_q_is[b,i,:,:] = W_out(i) zst_i + b_out(i) and the masked sum z_q on
+//                        the matrix cores (32-channel x 32-frame tiles, bias as a 9th k): the
+//                        HBM write stream, with no LDS and a few VALU per element.
+//
+// Codes of every golden fixture are reproduced bit for bit (the same fp32 expression for the
+// distance as the reference: dot in k order, fma(d, -2, e2) + c2, lowest index on ties).
 #include "common.h"
 #include "lanes.h"
-#include <stdlib.h>
 
 namespace {
 
-constexpr int RVQ_THREADS = 256;
-constexpr int RVQ_D = 1024;     // latent channels (all conf/*.yml)
-constexpr int RVQ_CPT = RVQ_D / RVQ_THREADS;
-constexpr int RVQ_CD = 8;       // codebook_dim
+constexpr int RD = 1024;        // latent channels
+constexpr int RCD = 8;          // codebook_dim
+constexpr int PJ_SPLIT = 8;     // channel splits of the projection GEMM
+constexpr int PJ_CPS = RD / PJ_SPLIT;
+constexpr int PJ_TC = 96;       // frames per projection tile (6 MFMA column tiles)
+constexpr int PJ_ZLD = 112;     // z_s row stride (== 16 mod 32: conflict-free B reads)
+constexpr int PJ_WLD = 80;      // w_s row stride (== 16 mod 32: conflict-free A reads)
+constexpr int CH_NT = 512;      // chain threads (8 waves)
+constexpr int CH_NW = CH_NT / 64;
+constexpr int CH_FMAX = 16;     // frames per chain workgroup
+constexpr int CH_NQMAX = 32;
 
-struct CodesArgs {
-  const float* z;
-  int B, T, nq, N;
-  const float* w_in_t;  // [nq][D][8]
-  const float* b_in;    // [nq][8]
-  const float* cb;      // [nq][N][8]
-  const float* cbn;     // [nq][N][8]
-  const float* c2;      // [nq][N]
-  const float* w_out;   // [nq][D][8]
-  const float* b_out;   // [nq][D]
-  int64_t* codes;       // [B][nq][T]
-  float* latents;       // [B][nq*8][T]
-  float* loss_pf;       // [B][nq][T]
-  float* zst;           // [B][nq][T][8]
-  unsigned long long* stamps;  // diagnostic build only (-DVRVQ_STAMPS): [blocks][nq][8]
-};
-
-#ifdef VRVQ_STAMPS
-#define STAMP(step)                                                                   \
-  do {                                                                                \
-    if (a.stamps && threadIdx.x == 0) {                                               \
-      unsigned long long t_;                                                          \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
-      a.stamps[((size_t)blockIdx.x * a.nq + i) * 8 + (step)] = t_;                   \
-    }                                                                                 \
-  } while (0)
-#else
-#define STAMP(step) do {} while (0)
-#endif
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// Workgroup = FG frame groups x 4 frames (FG * 256 threads; FG is chosen so that there is about
-// one workgroup per CU). Thread (g, t) owns latent channels c = t + 256 j (j < 4) of the 4
-// frames of group g: 16 residual VGPRs, and every weight it reads is reused 4 times from a
-// register. Stage weights (normalised codebook, c2, W_out, b_out: 72 KB; raw codebook 32 KB,
-// double-buffered) are copied to LDS by LDS-DMA, each buffer re-issued for the next stage right
-// after its last read, so the copies land during the rest of the stage; W_in comes through
-// registers, prefetched one stage ahead. Two workgroup barriers per stage:
-//   in_proj (packed FMA) -> wave reduce-scatter (permlane/DPP) -> [A] ->
-//   every wave: z_e, L2-normalise, distance scan over its codes n = t + 256 m, argmin
-//   reduce-scatter -> [B] -> every wave: final argmin, codeword, loss, straight-through vector,
-//   out_proj + residual update.
-// Wave-uniform vectors (e, zst of the group's frames) are broadcast through a per-wave LDS slot.
-constexpr int RVQ_FPG = 4;  // frames per group
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-// LDS-DMA of `nchunks` 1-KiB chunks src -> dst, chunk q issued by wave q % nwaves.
-__device__ __forceinline__ void dma_chunks(const float* src, float* dst, int nchunks, int wave,
-                                           int nwaves, int lane) {
-  for (int q = wave; q < nchunks; q += nwaves)
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(src + q * 256 + lane * 4),
-        (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
-}
-
-template <int FG, int NM>
-__global__ __launch_bounds__(RVQ_THREADS * FG) void rvq_codes_kernel(CodesArgs a) {
-  // NM = codes per thread = N / 256 (compile-time: the scan below is branch-free)
-  constexpr int F = FG * RVQ_FPG;          // frames per workgroup
-  constexpr int NTH = RVQ_THREADS * FG;
-  constexpr int NW = NTH / 64;             // waves
-  constexpr int N = NM * RVQ_THREADS;      // codebook size
-  // LDS (floats). Small arrays first (immediate ds offsets stay < 64 KiB):
-  //   red [FG][4][32] | db, ib [FG][4][4] | wv [NW][40] per-wave broadcast slot
-  //   cbn [N][8] | c2 [N] | wo [D][8] | bo [D] | raw [2][N][8]
-  constexpr int SMALL = FG * 128 + 2 * FG * 16 + NW * 40;
-  constexpr int BIG = N * RVQ_CD + N + RVQ_D * RVQ_CD + RVQ_D + 2 * N * RVQ_CD;
-  static_assert(BIG >= RVQ_D * F, "residual transpose fits the weight area");
-  __shared__ __attribute__((aligned(16))) float smem[SMALL + BIG];
-  float* red = smem;
-  float* db = red + FG * 128;
-  int* ib = reinterpret_cast<int*>(db + FG * 16);
-  float* wv_all = reinterpret_cast<float*>(ib + FG * 16);
-  float* big = smem + SMALL;
-  float* cbn_s = big;
-  float* c2_s = cbn_s + N * RVQ_CD;
-  float* wo_s = c2_s + N;
-  float* bo_s = wo_s + RVQ_D * RVQ_CD;
-  float* raw_s = bo_s + RVQ_D;  // [2][N][8]
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = wave >> 2;             // frame group
-  const int wg = wave & 3;             // wave inside the group
-  const int ct = tid & (RVQ_THREADS - 1);
-  const int NF = a.B * a.T;
-  const int n0 = blockIdx.x * F;
-  float* wv = wv_all + wave * 40;      // this wave's broadcast slot: [32] vector + [4] extra
-
-  // ---- residual tile z[b, :, t] through LDS (lanes frame-fastest) ----
-  {
-    const int f = tid % F;
-    const int n = n0 + f;
-    const bool valid = n < NF;
-    const int b = valid ? n / a.T : 0;
-    const int t = valid ? n - b * a.T : 0;
-    const float* zb = a.z + (size_t)b * RVQ_D * a.T + t;
-    for (int c = tid / F; c < RVQ_D; c += NTH / F)
-      big[c * F + f] = valid ? zb[(size_t)c * a.T] : 0.0f;
-  }
-  __syncthreads();
-  float r[RVQ_CPT][RVQ_FPG];
-#pragma unroll
-  for (int j = 0; j < RVQ_CPT; ++j)
-#pragma unroll
-    for (int f = 0; f < RVQ_FPG; ++f) r[j][f] = big[(ct + RVQ_THREADS * j) * F + g * RVQ_FPG + f];
-  __syncthreads();  // the transpose area becomes the weight buffers
-
-  // stage-0 codebooks (W_out / b_out are fetched inside the stage, after barrier A)
-  dma_chunks(a.cbn, cbn_s, N * RVQ_CD / 256, wave, NW, lane);
-  dma_chunks(a.c2, c2_s, N / 256, wave, NW, lane);
-  dma_chunks(a.cb, raw_s, N * RVQ_CD / 256, wave, NW, lane);
-
-  // per-lane frame/k of the (frame, k) epilogue: lanes l and l^32 mirror each other
-  const int ef = (lane >> 3) & 3, ek = lane & 7;
-  const int en = n0 + g * RVQ_FPG + ef;
-  const bool estore = (wg == 0) && (lane < 32) && en < NF;
-  const int eb = en < NF ? en / a.T : 0;
-  const int et = en < NF ? en - eb * a.T : 0;
-
-  float4 wi[RVQ_CPT][2];
-#pragma unroll
-  for (int j = 0; j < RVQ_CPT; ++j) {
-    const float* wp = a.w_in_t + (size_t)(ct + RVQ_THREADS * j) * RVQ_CD;
-    wi[j][0] = ld4(wp);
-    wi[j][1] = ld4(wp + 4);
-  }
-
-  for (int i = 0; i < a.nq; ++i) {
-    const bool more = i + 1 < a.nq;
-    STAMP(0);
-    // (1) in_proj partials p[f*8 + k] = sum_j W_in[k, c_j] r[c_j, f]  (v_pk_fma_f32 over k pairs)
-    float p[32];
-    {
-      f2 pp[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) pp[q] = f2{0.0f, 0.0f};
-#pragma unroll
-      for (int j = 0; j < RVQ_CPT; ++j) {
-        const f2 w01 = {wi[j][0].x, wi[j][0].y}, w23 = {wi[j][0].z, wi[j][0].w};
-        const f2 w45 = {wi[j][1].x, wi[j][1].y}, w67 = {wi[j][1].z, wi[j][1].w};
-#pragma unroll
-        for (int f = 0; f < RVQ_FPG; ++f) {
-          const f2 rr = {r[j][f], r[j][f]};
-          pp[f * 4 + 0] = __builtin_elementwise_fma(w01, rr, pp[f * 4 + 0]);
-          pp[f * 4 + 1] = __builtin_elementwise_fma(w23, rr, pp[f * 4 + 1]);
-          pp[f * 4 + 2] = __builtin_elementwise_fma(w45, rr, pp[f * 4 + 2]);
-          pp[f * 4 + 3] = __builtin_elementwise_fma(w67, rr, pp[f * 4 + 3]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        p[2 * q] = pp[q].x;
-        p[2 * q + 1] = pp[q].y;
-      }
+// ------------------------------------------------------------------------------------------
+// Prep (once per weight version, like the weight-norm fold):
+//   mcol[j][i][k][m] = sum_c W_in(i)[k][c] W_out(j)[c][m] for i > j (else 0)
+//   qb[i][k]         = sum_c W_in(i)[k][c] (sum_{j<i} b_out(j)[c])   (bias sum in stage order)
+__global__ void cross_prep_kernel(const float* __restrict__ w_in_t,  // [nq][D][8]
+                                  const float* __restrict__ w_out,   // [nq][D][8]
+                                  const float* __restrict__ b_out,   // [nq][D]
+                                  int nq, float* __restrict__ mcol, float* __restrict__ qb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nm = nq * nq * 64;
+  if (e < nm) {
+    const int m = e & 7, k = (e >> 3) & 7, ij = e >> 6;
+    const int i = ij % nq, j = ij / nq;
+    float acc = 0.0f;
+    if (i > j) {
+      const float* wi = w_in_t + (size_t)i * RD * RCD + k;
+      const float* wo = w_out + (size_t)j * RD * RCD + m;
+      for (int c = 0; c < RD; ++c) acc = fmaf(wi[c * RCD], wo[c * RCD], acc);
     }
-    STAMP(1);
-    // (2) wave reduce-scatter: lanes l, l^32 <- wave sum of p[l & 31]
-    {
-      const float v = vrvq::reduce_scatter32(p, lane);
-      if (lane < 32) red[(g * 4 + wg) * 32 + lane] = v;
+    mcol[e] = acc;
+  } else if (e < nm + nq * RCD) {
+    const int q = e - nm, i = q / RCD, k = q % RCD;
+    const float* wi = w_in_t + (size_t)i * RD * RCD + k;
+    float acc = 0.0f;
+    for (int c = 0; c < RD; ++c) {
+      float bs = 0.0f;
+      for (int j = 0; j < i; ++j) bs = bs + b_out[(size_t)j * RD + c];
+      acc = fmaf(wi[c * RCD], bs, acc);
     }
-    const float bin = a.b_in[i * RVQ_CD + ek];
-    STAMP(2);
-    // this stage's codebook LDS-DMA (issued after barrier B of the previous stage) landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // ---------------------------------------------------------------- A
-    STAMP(3);
-    // this stage's W_out / b_out (the buffer's last reads, out_proj of stage i-1, precede A)
-    dma_chunks(a.w_out + (size_t)i * RVQ_D * RVQ_CD, wo_s, RVQ_D * RVQ_CD / 256, wave, NW, lane);
-    dma_chunks(a.b_out + (size_t)i * RVQ_D, bo_s, RVQ_D / 256, wave, NW, lane);
-    if (more) {  // next stage's W_in into registers
-#pragma unroll
-      for (int j = 0; j < RVQ_CPT; ++j) {
-        const float* wp = a.w_in_t + ((size_t)(i + 1) * RVQ_D + ct + RVQ_THREADS * j) * RVQ_CD;
-        wi[j][0] = ld4(wp);
-        wi[j][1] = ld4(wp + 4);
-      }
-    }
-    // (3) z_e and its L2 normalisation, computed by every wave for its group's frames
-    //     (lane = f*8 + k; lanes 32..63 mirror 0..31)
-    float ze, e, e2;
-    {
-      const float* rr = red + g * 128 + (lane & 31);
-      ze = ((rr[0] + rr[32]) + (rr[64] + rr[96])) + bin;
-      const float n2 = vrvq::sum8(ze * ze, lane);
-      e = ze / fmaxf(sqrtf(n2), 1e-12f);
-      e2 = vrvq::sum8(e * e, lane);
-      if (estore) a.latents[((size_t)eb * a.nq * RVQ_CD + i * RVQ_CD + ek) * a.T + et] = ze;
-    }
-    // broadcast e (k-major, frames interleaved) and e2 through this wave's LDS slot
-    if (lane < 32) wv[ek * RVQ_FPG + ef] = e;
-    if (lane < 32 && ek == 0) wv[32 + ef] = e2;
-    STAMP(4);
-    // (4) nearest codeword over this thread's codes (lowest index on ties)
-    float best[RVQ_FPG];
-    int bidx[RVQ_FPG];
-    {
-      f2 e01[RVQ_CD], e23[RVQ_CD];
-#pragma unroll
-      for (int k = 0; k < RVQ_CD; ++k) {
-        const float4 ek4 = *reinterpret_cast<const float4*>(wv + k * RVQ_FPG);
-        e01[k] = f2{ek4.x, ek4.y};
-        e23[k] = f2{ek4.z, ek4.w};
-      }
-      const float4 e2v = *reinterpret_cast<const float4*>(wv + 32);
-      const f2 e2a = {e2v.x, e2v.y}, e2b = {e2v.z, e2v.w};
-#pragma unroll
-      for (int f = 0; f < RVQ_FPG; ++f) {
-        best[f] = INFINITY;
-        bidx[f] = 0x7fffffff;
-      }
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int n = ct + RVQ_THREADS * m;
-        const float4 c0 = *reinterpret_cast<const float4*>(cbn_s + n * RVQ_CD);
-        const float4 c1 = *reinterpret_cast<const float4*>(cbn_s + n * RVQ_CD + 4);
-        const float ck[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        // dot in k order (mul, then fma chain): bit-identical to dot8 per frame
-        f2 da = e01[0] * f2{ck[0], ck[0]}, dbb = e23[0] * f2{ck[0], ck[0]};
-#pragma unroll
-        for (int k = 1; k < RVQ_CD; ++k) {
-          da = __builtin_elementwise_fma(e01[k], f2{ck[k], ck[k]}, da);
-          dbb = __builtin_elementwise_fma(e23[k], f2{ck[k], ck[k]}, dbb);
-        }
-        // (sum e^2 - 2 e.c) + sum c^2   (models/quantize.py:96-100)
-        const float cc = c2_s[n];
-        const f2 dA = (e2a - 2.0f * da) + f2{cc, cc};
-        const f2 dB = (e2b - 2.0f * dbb) + f2{cc, cc};
-        const float dv[4] = {dA.x, dA.y, dB.x, dB.y};
-#pragma unroll
-        for (int f = 0; f < RVQ_FPG; ++f) {
-          const bool take = dv[f] < best[f];  // n increasing: strict < keeps the first
-          best[f] = take ? dv[f] : best[f];
-          bidx[f] = take ? n : bidx[f];
-        }
-      }
-    }
-    vrvq::argmin_scatter4(best, bidx, lane);
-    if ((lane & 15) == 0) {
-      db[(g * 4 + wg) * 4 + (lane >> 4)] = best[0];
-      ib[(g * 4 + wg) * 4 + (lane >> 4)] = bidx[0];
-    }
-    STAMP(5);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W_out / b_out DMA (issued after A) landed
-    __syncthreads();  // ---------------------------------------------------------------- B
-    STAMP(6);
-    if (more) {  // next stage's cbn / c2 / raw codebook (this stage's cbn / c2 reads are done;
-                 // the other raw buffer was last read a stage ago)
-      dma_chunks(a.cbn + (size_t)(i + 1) * N * RVQ_CD, cbn_s, N * RVQ_CD / 256, wave, NW, lane);
-      dma_chunks(a.c2 + (size_t)(i + 1) * N, c2_s, N / 256, wave, NW, lane);
-      dma_chunks(a.cb + (size_t)(i + 1) * N * RVQ_CD, raw_s + ((i + 1) & 1) * N * RVQ_CD,
-                 N * RVQ_CD / 256, wave, NW, lane);
-    }
-    // (5) final argmin, codeword, per-frame loss, straight-through vector (every wave)
-    {
-      float bd = db[(g * 4) * 4 + ef];
-      int bi = ib[(g * 4) * 4 + ef];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) vrvq::amin(bd, bi, db[(g * 4 + w) * 4 + ef], ib[(g * 4 + w) * 4 + ef]);
-      const float zq = raw_s[(i & 1) * N * RVQ_CD + bi * RVQ_CD + ek];
-      const float st = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
-      if (lane < 32) wv[ek * RVQ_FPG + ef] = st;
-      if (wg == 0) {
-        const float diff = ze - zq;
-        const float l2 = vrvq::sum8(diff * diff, lane);
-        if (estore) {
-          const size_t fo = ((size_t)eb * a.nq + i) * a.T + et;
-          a.zst[fo * RVQ_CD + ek] = st;
-          if (ek == 0) {
-            a.codes[fo] = (int64_t)bi;
-            a.loss_pf[fo] = l2 / 8.0f;
-          }
-        }
-      }
-    }
-    STAMP(7);
-    // (6) out_proj + residual update: r[c, f] -= W_out[c, :] . zst[f] + b_out[c]
-    {
-      float4 wo[RVQ_CPT][2];
-      float bo[RVQ_CPT];
-#pragma unroll
-      for (int j = 0; j < RVQ_CPT; ++j) {
-        const int c = ct + RVQ_THREADS * j;
-        wo[j][0] = *reinterpret_cast<const float4*>(wo_s + c * RVQ_CD);
-        wo[j][1] = *reinterpret_cast<const float4*>(wo_s + c * RVQ_CD + 4);
-        bo[j] = bo_s[c];
-      }
-      f2 z01[RVQ_CD], z23[RVQ_CD];
-#pragma unroll
-      for (int k = 0; k < RVQ_CD; ++k) {
-        const float4 zk = *reinterpret_cast<const float4*>(wv + k * RVQ_FPG);
-        z01[k] = f2{zk.x, zk.y};
-        z23[k] = f2{zk.z, zk.w};
-      }
-#pragma unroll
-      for (int j = 0; j < RVQ_CPT; ++j) {
-        const float wk[8] = {wo[j][0].x, wo[j][0].y, wo[j][0].z, wo[j][0].w,
-                             wo[j][1].x, wo[j][1].y, wo[j][1].z, wo[j][1].w};
-        // out_proj1 per frame: (w0*z0, fma chain over k) + bias -- packed over frame pairs
-        f2 qa = f2{wk[0], wk[0]} * z01[0], qb = f2{wk[0], wk[0]} * z23[0];
-#pragma unroll
-        for (int k = 1; k < RVQ_CD; ++k) {
-          qa = __builtin_elementwise_fma(f2{wk[k], wk[k]}, z01[k], qa);
-          qb = __builtin_elementwise_fma(f2{wk[k], wk[k]}, z23[k], qb);
-        }
-        qa = qa + f2{bo[j], bo[j]};
-        qb = qb + f2{bo[j], bo[j]};
-        r[j][0] = r[j][0] - qa.x;
-        r[j][1] = r[j][1] - qa.y;
-        r[j][2] = r[j][2] - qb.x;
-        r[j][3] = r[j][3] - qb.y;
-      }
-    }
-    // LDS hazards: red (written before A of the next stage) was last read before B here; db/ib
-    // (written before B) were last read before A; wv is wave-private.
+    qb[q] = acc;
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// Expansion: lane = frame (flattened b*T + t, 256 per workgroup), workgroup also owns CB
-// latent channels. For each stage the lane loads its frame's 8-float straight-through vector
-// once; each channel's W_out row is wave-uniform and comes through the scalar cache. Every
-// store instruction writes 64 consecutive frames of one channel row (256 B), so the z_q_is
-// stream is written at full coalescing; z_q accumulates the masked sum in registers in stage
-// order (models/quantize.py:420-421).
-struct ExpandArgs {
-  const float* zst;     // [B][nq][T][8]
-  int B, D, T, nq;
-  const float* w_out;   // [nq][D][8]
-  const float* b_out;   // [nq][D]
-  const float* imp;     // [B][T] or null (CBR: mask = 1)
-  float level;
-  float* z_q_is;        // [B][nq][D][T] or null
-  float* z_q;           // [B][D][T]
-  float* mask;          // [B][nq][T] or null
-  int n_cc;             // channel chunks
-};
-
-constexpr int EXP_THREADS = 256;
-constexpr int EXP_CB = 16;  // channels per workgroup
-
-__global__ __launch_bounds__(EXP_THREADS) void rvq_expand_kernel(
-    ExpandArgs a, const float* __restrict__ zst_g, const float* __restrict__ w_out,
-    const float* __restrict__ b_out, const float* __restrict__ imp_g, float* __restrict__ z_q_is,
-    float* __restrict__ z_q, float* __restrict__ mask) {
-  // All pointers are distinct buffers (restrict): lets the compiler keep the wave-uniform
-  // weight loads on the scalar path ahead of the stores.
-  const int cc = blockIdx.x % a.n_cc;
-  const int fc = blockIdx.x / a.n_cc;
-  const int c0 = cc * EXP_CB;
-  const int NF = a.B * a.T;
-  const int n = fc * EXP_THREADS + threadIdx.x;
-  const bool valid = n < NF;
-  const int b = valid ? n / a.T : 0;
-  const int t = valid ? n - b * a.T : 0;
-  const float s = (imp_g && valid) ? (imp_g[n] * a.level) * (float)a.nq : INFINITY;
-
-  // This workgroup's W_out rows / biases for every stage: [nq][CB][8] then [nq][CB].
-  extern __shared__ __attribute__((aligned(16))) float w_s[];
-  for (int e = threadIdx.x; e < a.nq * EXP_CB * 2; e += EXP_THREADS) {
-    const int i = e / (EXP_CB * 2), r = e - i * (EXP_CB * 2);
-    reinterpret_cast<float4*>(w_s)[e] =
-        *reinterpret_cast<const float4*>(w_out + ((size_t)i * a.D + c0) * RVQ_CD + r * 4);
-  }
-  for (int e = threadIdx.x; e < a.nq * EXP_CB; e += EXP_THREADS) {
-    const int i = e / EXP_CB, q = e - i * EXP_CB;
-    w_s[a.nq * EXP_CB * RVQ_CD + e] = b_out[(size_t)i * a.D + c0 + q];
-  }
-  __syncthreads();
-
-  float acc[EXP_CB];
-#pragma unroll
-  for (int q = 0; q < EXP_CB; ++q) acc[q] = 0.0f;
-
-  for (int i = 0; i < a.nq; ++i) {
-    float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), z1 = z0;
-    if (valid) {
-      const float* zp = zst_g + (((size_t)b * a.nq + i) * a.T + t) * RVQ_CD;
-      z0 = ld4(zp);
-      z1 = ld4(zp + 4);
-    }
-    const float m = (s - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
-    if (mask && cc == 0 && valid) mask[((size_t)b * a.nq + i) * a.T + t] = m;
-    float* dst = z_q_is ? z_q_is + (((size_t)b * a.nq + i) * a.D + c0) * a.T + t : nullptr;
-    // Wave-uniform weight rows: LDS broadcast reads.
-    const float* wrow = w_s + i * EXP_CB * RVQ_CD;
-    const float* brow = w_s + a.nq * EXP_CB * RVQ_CD + i * EXP_CB;
-    float v[EXP_CB];
-#pragma unroll
-    for (int q = 0; q < EXP_CB; ++q) {
-      const float4 w0 = *reinterpret_cast<const float4*>(wrow + q * RVQ_CD);
-      const float4 w1 = *reinterpret_cast<const float4*>(wrow + q * RVQ_CD + 4);
-      v[q] = out_proj1(w0, w1, brow[q], z0, z1);
-      acc[q] = acc[q] + v[q] * m;
-    }
-    if (dst && valid) {
-#pragma unroll
-      for (int q = 0; q < EXP_CB; ++q) dst[(size_t)q * a.T] = v[q];
-    }
-  }
-  if (valid) {
-    float* zq = z_q + ((size_t)b * a.D + c0) * a.T + t;
-#pragma unroll
-    for (int q = 0; q < EXP_CB; ++q) zq[(size_t)q * a.T] = acc[q];
+// Prep: the normalised codebooks in the chain's MFMA A-fragment order, so that every lane loads
+// its stage operands as contiguous float4:
+//   cbf[i][w][l][t][kh] = cbn[i][w*N/8 + 16 t + (l & 15)][4 kh + (l >> 4)]
+// (wave w of the chain owns codes [w N/8, (w+1) N/8) as N/128 tiles of 16 codes).
+__global__ void rvq_frag_kernel(const float* __restrict__ cbn, int nq, int N,
+                                float* __restrict__ cbf) {
+  const size_t total = (size_t)nq * N * RCD;
+  const int NT = N / 128;
+  for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < total;
+       o += (size_t)gridDim.x * blockDim.x) {
+    const int kh = (int)(o % 2);
+    size_t r = o / 2;
+    const int t = (int)(r % NT);
+    r /= NT;
+    const int l = (int)(r % 64);
+    r /= 64;
+    const int w = (int)(r % CH_NW);
+    const int i = (int)(r / CH_NW);
+    const int code = w * (N / CH_NW) + 16 * t + (l & 15);
+    cbf[o] = cbn[((size_t)i * N + code) * RCD + 4 * kh + (l >> 4)];
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// Projection: part[s][n][r] = sum_{c in split s} W_in_t[r/8][c][r%8] z[b][c][t], n = b*T + t,
+// r < R = nq*8. Workgroup = (clip b, frame tile of <= 96, channel split s, 64-row block), 8
+// waves: wave w computes rows 16 (w & 3) .. +15 for column tiles 3 (w >> 2) .. +2 with
+// v_mfma_f32_16x16x4_f32. K = 128 channels in 4 chunks of 32, double-buffered in LDS: the
+// [32 ch][96 t] slab of z (row segments of one clip, coalesced) and the [32][64] weight block
+// of chunk c+1 are loaded into registers while the MFMAs consume chunk c. Output: lane l holds
+// 4 consecutive rows of one frame -> one float4 store.
+constexpr int PJ_NT = 512;
+constexpr int PJ_KC = 32;                       // channels per K chunk
+constexpr int PJ_ZQ = PJ_KC * PJ_TC / PJ_NT;    // z loads per thread per chunk (6)
+constexpr int PJ_STG = PJ_KC * PJ_ZLD + PJ_KC * PJ_WLD;
+
+__global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restrict__ z, int T,
+                                                            int nq, int n_tc,
+                                                            const float* __restrict__ w_in_t,
+                                                            float* __restrict__ part, int NF) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * PJ_STG];
+  const int tc = blockIdx.x % n_tc, b = blockIdx.x / n_tc;
+  const int s = blockIdx.y, rb = blockIdx.z;
+  const int R = nq * RCD;
+  const int t0 = tc * PJ_TC;
+  const int ntl = min(PJ_TC, T - t0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
+  float zv[PJ_ZQ];
+  float4 wv;
+  auto load = [&](int kc) {  // chunk kc -> registers
+#pragma unroll
+    for (int q = 0; q < PJ_ZQ; ++q) {
+      const int e = tid + PJ_NT * q;
+      const int c = e / PJ_TC, t = e - c * PJ_TC;
+      zv[q] = t < ntl ? zb[(size_t)(kc * PJ_KC + c) * T + t] : 0.0f;
+    }
+    // 8 stages x 32 channels x 2 float4 = one float4 per thread
+    const int sl = tid >> 6, rem = tid & 63;
+    const int st = rb * 8 + sl;
+    wv = st < nq ? ld4(w_in_t + ((size_t)st * RD + s * PJ_CPS + kc * PJ_KC) * RCD + rem * 4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store = [&](float* stg) {
+    float* z_s = stg;
+    float* w_s = stg + PJ_KC * PJ_ZLD;
+#pragma unroll
+    for (int q = 0; q < PJ_ZQ; ++q) {
+      const int e = tid + PJ_NT * q;
+      const int c = e / PJ_TC, t = e - c * PJ_TC;
+      z_s[c * PJ_ZLD + t] = zv[q];
+    }
+    const int sl = tid >> 6, rem = tid & 63;
+    *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) = wv;
+  };
+  const int rt = wave & 3, cg = wave >> 2;
+  const int lr = lane & 15, lk = lane >> 4;
+  f32x4 acc[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(sm);
+  __syncthreads();
+#pragma unroll 1
+  for (int kc = 0; kc < PJ_CPS / PJ_KC; ++kc) {
+    const bool more = kc + 1 < PJ_CPS / PJ_KC;
+    if (more) load(kc + 1);  // in flight during the MFMAs below
+    const float* z_s = sm + (kc & 1) * PJ_STG;
+    const float* w_s = z_s + PJ_KC * PJ_ZLD;
+    // all column tiles unconditionally (zero-padded frames): a runtime-guarded MFMA makes the
+    // compiler shuffle the accumulators through v_mov / accvgpr copies every step
+#pragma unroll
+    for (int kk = 0; kk < PJ_KC / 4; ++kk) {
+      const int c = kk * 4 + lk;
+      const float av = w_s[c * PJ_WLD + rt * 16 + lr];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float bv = z_s[c * PJ_ZLD + (cg * 3 + j) * 16 + lr];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) store(sm + ((kc + 1) & 1) * PJ_STG);
+    __syncthreads();
+  }
+  const int r0 = rb * 64 + rt * 16;
+  if (r0 >= R) return;
+  // D layout: lane l, reg q -> row 4*(l>>4) + q of the wave's 16, column (frame) l & 15
+  const int rr = r0 + 4 * lk;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int t = (cg * 3 + j) * 16 + lr;
+    if (t < ntl) {
+      const size_t n = (size_t)b * T + t0 + t;
+      *reinterpret_cast<float4*>(part + ((size_t)s * NF + n) * R + rr) =
+          make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// The chain. Workgroup = frames [n0, n0 + nf) of the flattened (b, t) axis, nf <= 16; 8 waves.
+//
+// Stage i, S1 (all waves):
+//   - deferred U updates: pu[f][ip] -= M_{ip,i-1} zst_{i-1} for ip > i (spread over all threads;
+//     ip = i was done on the critical path in S2 of stage i-1);
+//   - distance scan on the matrix cores: wave w owns codes [w N/8, (w+1) N/8) as 16-code tiles;
+//     D[code][frame] = cbn . e by two v_mfma_f32_16x16x4_f32 per tile (k = 0..3, then 4..7 on
+//     the same accumulator: the k-ordered fma chain of the reference's dot, bitwise), then per
+//     lane dist = fma(D, -2, e2) + c2 over its 32 (code, frame) entries in code order, and a
+//     lexicographic (dist, code) min across the 4 lanes of each frame -> per-wave candidate;
+//   - per wave and frame, the candidate's raw codebook row (gathered from L2 into LDS);
+//   - prefetches of stage i+1 (cbn fragments -> registers; c2 slice and M_{.,i+1} ->
+//     registers, stored to LDS at the start of stage i+1).
+// S2 (lanes (f, k), f < nf, tid = 8 f + k): cross-wave argmin (wave order = code order, lowest
+// code on ties), the winner's raw codeword, loss, zst, the next stage's pu[f][i+1] and z_e.
+// One workgroup per CU: F = ceil(B*T / 256) frames each (<= 16).
+// Two barriers per stage; outputs stay in LDS until the epilogue.
+struct ChainArgs {
+  const float* part;   // [8][NF][nq*8]
+  int B, T, nq, F, NF;
+  const float* b_in;   // [nq][8]
+  const float* qb;     // [nq][8]
+  const float* mcol;   // [nq][nq][8][8]
+  const float* cb;     // [nq][N][8]
+  const float* cbf;    // [nq][8][64][N/128][2] normalised codebook, fragment order
+  const float* c2;     // [nq][N]
+  const float* imp;    // [B][T] or null
+  float level;
+  int64_t* codes;      // [B][nq][T]
+  float* latents;      // [B][nq*8][T]
+  float* loss_pf;      // [B][nq][T]
+  float* zst;          // [B][nq][T][8]
+  float* mask;         // [B][nq][T] or null
+  unsigned long long* stamps;  // diagnostic build only (-DVRVQ_STAMPS): [grid][nq + 1][2][8]
+};
+
+#ifdef VRVQ_STAMPS
+// In-kernel s_memtime stamps (diagnostic build): lanes 0 of waves 0 and 7 record 8 points per
+// stage into a buffer nothing else reads.
+#define CSTAMP(stage, step)                                                                  \
+  do {                                                                                     \
+    if (a.stamps && (tid == 0 || tid == 448)) {                                            \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
+      a.stamps[(((size_t)blockIdx.x * (a.nq + 1) + (stage)) * 2 + (tid ? 1 : 0)) * 8 +      \
+               (step)] = t_;                                                               \
+    }                                                                                      \
+  } while (0)
+#else
+#define CSTAMP(stage, step) do {} while (0)
+#endif
+
+// LDS carve (floats), shared by the launcher's size computation.
+struct ChainLds {
+  int e, e2, cd, ci, cr, pu, lat, zs, code, loss, c2, m, total;
+  __host__ __device__ ChainLds(int nq, int F, int N) {
+    auto al = [](int x) { return (x + 3) & ~3; };
+    int o = 0;
+    e = o; o += al(CH_FMAX * RCD);
+    e2 = o; o += al(CH_FMAX);
+    cd = o; o += al(CH_FMAX * CH_NW);
+    ci = o; o += al(CH_FMAX * CH_NW);
+    cr = o; o += al(CH_FMAX * CH_NW * RCD);
+    pu = o; o += al(F * nq * RCD);
+    lat = o; o += al(F * nq * RCD);
+    zs = o; o += al(F * nq * RCD);
+    code = o; o += al(F * nq);
+    loss = o; o += al(F * nq);
+    c2 = o; o += al(2 * N);
+    m = o; o += al(3 * nq * 64);
+    total = o;
+  }
+};
+
+template <int NM>
+__global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
+  constexpr int N = 256 * NM;
+  constexpr int NPW = N / CH_NW;   // codes per wave
+  constexpr int NT = NPW / 16;     // 16-code MFMA tiles per wave
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int nq = a.nq, F = a.F;
+  const ChainLds L(nq, F, N);
+  float* e_s = sm + L.e;
+  float* e2_s = sm + L.e2;
+  float* cd_s = sm + L.cd;
+  int* ci_s = reinterpret_cast<int*>(sm + L.ci);
+  float* cr_s = sm + L.cr;      // [16][8 waves][8]: raw codebook row of each wave's candidate
+  float* pu_s = sm + L.pu;      // [F][nq][8]: ((P + b_in) - Qb) - U
+  float* lat_s = sm + L.lat;    // [F][nq][8]: z_e (output)
+  float* zs_s = sm + L.zs;      // [F][nq][8]: zst (output, and the U updates' input)
+  int* code_s = reinterpret_cast<int*>(sm + L.code);
+  float* loss_s = sm + L.loss;
+  float* c2_s = sm + L.c2;      // [2][N]
+  float* m_s = sm + L.m;        // [3][nq][8][8]: M_{.,j} for j = i-1, i, i+1 (mod 3)
+
+  const int n0 = blockIdx.x * F;
+  const int nf = min(F, a.NF - n0);
+  const int R = nq * RCD;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rf = tid >> 3, rk = tid & 7;  // S2 roles: (frame, k)
+  const bool role = rf < nf;
+  const int fl = lane & 15, lg = lane >> 4;  // MFMA roles: frame column, k / row group
+  const int cw = wave * NPW;
+  CSTAMP(nq, 0);
+
+  // ---- prologue: pu = (P + b_in) - Qb (partials summed in split order); stage 0 operands.
+  // Two (frame, row) items per thread per pass with all 16 partial loads in flight.
+  for (int e0 = tid; e0 < nf * R; e0 += 2 * CH_NT) {
+    float v[2][PJ_SPLIT];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = e0 + h * CH_NT;
+      const size_t base = (size_t)n0 * R + (e < nf * R ? e : 0);
+#pragma unroll
+      for (int sp = 0; sp < PJ_SPLIT; ++sp) v[h][sp] = a.part[(size_t)sp * a.NF * R + base];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = e0 + h * CH_NT;
+      if (e < nf * R) {
+        const int r = e % R;
+        float pv = v[h][0];
+#pragma unroll
+        for (int sp = 1; sp < PJ_SPLIT; ++sp) pv = pv + v[h][sp];
+        pu_s[e] = (pv + a.b_in[r]) - a.qb[r];
+      }
+    }
+  }
+  for (int e = tid; e < CH_FMAX * RCD; e += CH_NT) e_s[e] = 0.0f;
+  for (int e = tid; e < CH_FMAX; e += CH_NT) e2_s[e] = 0.0f;
+  float av[NT][2];  // cbn fragments of the current stage: code cw + 16 t + fl, k = 4 kh + lg
+  auto load_a = [&](int i, float (&dst)[NT][2]) {  // NT / 2 contiguous float4 per lane
+    const float* src = a.cbf + (((size_t)i * CH_NW + wave) * 64 + lane) * (2 * NT);
+#pragma unroll
+    for (int q = 0; q < NT / 2; ++q) {
+      const float4 v = ld4(src + 4 * q);
+      dst[2 * q][0] = v.x; dst[2 * q][1] = v.y; dst[2 * q + 1][0] = v.z; dst[2 * q + 1][1] = v.w;
+    }
+  };
+  load_a(0, av);
+  for (int e = tid; e < N; e += CH_NT) c2_s[e] = a.c2[e];
+  if (nq > 1)
+    for (int e = tid; e < R * RCD / 4; e += CH_NT)
+      reinterpret_cast<float4*>(m_s)[e] = ld4(a.mcol + (size_t)e * 4);
+  __syncthreads();
+  float ze = 0.0f;  // S2 lanes: z_e of (rf, rk) at the current stage
+  auto set_e = [&](float zv) {  // F.normalize (eps 1e-12) of the 8-lane group's z_e
+    ze = zv;
+    const float n2 = vrvq::sum8(ze * ze, lane);
+    const float e = ze / fmaxf(sqrtf(n2), 1e-12f);
+    const float e2 = vrvq::sum8(e * e, lane);
+    if (role) {
+      e_s[rf * RCD + rk] = e;
+      if (rk == 0) e2_s[rf] = e2;
+    }
+  };
+  set_e(role ? pu_s[(rf * nq) * RCD + rk] : 0.0f);
+  __syncthreads();
+  CSTAMP(nq, 1);
+
+  // next stage's c2 slice / M column: loaded during a stage, stored to LDS at the start of the
+  // next (no wait on a load issued in the same stage)
+  constexpr int C2W = (NPW + 63) / 64;
+  float c2n[C2W];
+  float4 mn = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < nq; ++i) {
+    const bool more = i + 1 < nq;
+    // ---- S1 ----
+    CSTAMP(i, 0);
+    if (i > 0) {
+      // stage i operands prefetched during stage i-1: M_{.,i} (read by other waves after
+      // barrier 1) and this wave's c2 slice (read by this wave only)
+#pragma unroll
+      for (int q = 0; q < C2W; ++q)
+        if (lane + 64 * q < NPW) c2_s[(i & 1) * N + cw + lane + 64 * q] = c2n[q];
+      if (i + 1 < nq && tid * 4 < R * RCD)
+        reinterpret_cast<float4*>(m_s + (i % 3) * R * RCD)[tid] = mn;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the c2 slice is in LDS for the scan
+      // deferred U updates from stage i-1 for targets ip > i
+      const int nip = nq - 1 - i;
+      const float* mj = m_s + ((i - 1) % 3) * R * RCD;
+      for (int e = tid; e < nf * nip * RCD; e += CH_NT) {
+        const int k = e & 7, q = e >> 3;
+        const int f = q / nip, ip = i + 1 + (q - f * nip);
+        const float* zr = zs_s + (f * nq + (i - 1)) * RCD;
+        const float* mr = mj + (ip * RCD + k) * RCD;
+        float* pp = pu_s + (f * nq + ip) * RCD + k;
+        *pp = *pp - dot8(ld4(mr), ld4(mr + 4), ld4(zr), ld4(zr + 4));
+      }
+    }
+    CSTAMP(i, 1);
+    float an[NT][2];
+    CSTAMP(i, 2);
+    {
+      // distance scan: 16 frames x NT 16-code tiles, K = 8 as two k-quads. All MFMAs first
+      // (NT independent accumulators), c2 read before them; then 4 independent argmin chains
+      // (one per accumulator row r: codes cw + 16 t + 4 lg + r in increasing t) merged
+      // lexicographically (dist, code) -- the same result as one chain in code order.
+      const float b0 = e_s[fl * RCD + lg], b1 = e_s[fl * RCD + 4 + lg];
+      const float e2 = e2_s[fl];
+      const float* c2c = c2_s + (i & 1) * N + cw + 4 * lg;
+      float4 cc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) cc[t] = ld4(c2c + t * 16);
+      f32x4 d[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][0], b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, d[t], 0, 0, 0);
+      float bst[4];
+      int bix[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bst[r] = INFINITY;
+        bix[r] = cw + 4 * lg + r;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float ccv[4] = {cc[t].x, cc[t].y, cc[t].z, cc[t].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // (sum e^2 - 2 e.c) + sum c^2 with the first step as fma(d, -2, e2): 2d is exact,
+          // so this is the reference's rounding (models/quantize.py:96-100)
+          const float dist = fmaf(d[t][r], -2.0f, e2) + ccv[r];
+          const bool take = dist < bst[r];  // increasing code index: strict < keeps the first
+          bst[r] = take ? dist : bst[r];
+          bix[r] = take ? cw + t * 16 + 4 * lg + r : bix[r];
+        }
+      }
+      vrvq::amin(bst[0], bix[0], bst[1], bix[1]);
+      vrvq::amin(bst[2], bix[2], bst[3], bix[3]);
+      vrvq::amin(bst[0], bix[0], bst[2], bix[2]);
+      float best = bst[0];
+      int bidx = bix[0];
+      vrvq::amin(best, bidx, vrvq::xchg<16>(best, lane), vrvq::xchg<16>(bidx, lane));
+      vrvq::amin(best, bidx, vrvq::xchg<32>(best, lane), vrvq::xchg<32>(bidx, lane));
+      // the candidate's raw codebook row (L2 gather, models/quantize.py:101-103): only the
+      // wave's own candidates, so no per-stage staging of the whole raw codebook. Issued
+      // before the next stage's prefetch, so the wait for it does not cover the prefetch.
+      const float* row = a.cb + ((size_t)i * N + (lane < nf ? bidx : 0)) * RCD;
+      const float4 r0 = ld4(row), r1 = ld4(row + 4);
+      if (more) {  // stage i+1 operands (cbn fragments, c2 slice, M column)
+        load_a(i + 1, an);
+#pragma unroll
+        for (int q = 0; q < C2W; ++q)
+          c2n[q] = lane + 64 * q < NPW ? a.c2[(size_t)(i + 1) * N + cw + lane + 64 * q] : 0.0f;
+        if (i + 2 < nq && tid * 4 < R * RCD)  // M_{.,i+1}: needed from stage i+1 on
+          mn = ld4(a.mcol + (size_t)(i + 1) * R * RCD + tid * 4);
+      }
+      if (lane < nf) {
+        cd_s[lane * CH_NW + wave] = best;
+        ci_s[lane * CH_NW + wave] = bidx;
+        float* crw = cr_s + (lane * CH_NW + wave) * RCD;
+        *reinterpret_cast<float4*>(crw) = r0;
+        *reinterpret_cast<float4*>(crw + 4) = r1;
+      }
+    }
+    CSTAMP(i, 3);
+    __syncthreads();  // ------------------------------- candidates, stage i+1's c2 / M ready
+    CSTAMP(i, 4);
+    // ---- S2 (role lanes) ----
+    int bi = 0;
+    float zq = 0.0f;
+    if (role) {
+      const float4 d0 = ld4(cd_s + rf * CH_NW), d1 = ld4(cd_s + rf * CH_NW + 4);
+      const int4 i0 = *reinterpret_cast<const int4*>(ci_s + rf * CH_NW);
+      const int4 i1 = *reinterpret_cast<const int4*>(ci_s + rf * CH_NW + 4);
+      const float dv[CH_NW] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      const int iv[CH_NW] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+      float bd = dv[0];
+      bi = iv[0];
+      int bw = 0;
+#pragma unroll
+      for (int w = 1; w < CH_NW; ++w) {  // wave order = code order: strict < keeps the lowest
+        const bool take = dv[w] < bd;
+        bd = take ? dv[w] : bd;
+        bi = take ? iv[w] : bi;
+        bw = take ? w : bw;
+      }
+      bi = (bi >= 0 && bi < N) ? bi : 0;
+      zq = cr_s[(rf * CH_NW + bw) * RCD + rk];  // raw codebook row of the winner
+    }
+    const float zsv = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
+    const float diff = ze - zq;
+    const float l2 = vrvq::sum8(diff * diff, lane);
+    if (role) {
+      lat_s[(rf * nq + i) * RCD + rk] = ze;
+      zs_s[(rf * nq + i) * RCD + rk] = zsv;
+      if (rk == 0) {
+        code_s[rf * nq + i] = bi;
+        loss_s[rf * nq + i] = l2 / 8.0f;  // mse over codebook_dim, models/quantize.py:69-71
+      }
+    }
+    CSTAMP(i, 5);
+    if (more) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this group's zst row is in LDS
+      float zn = 0.0f;
+      if (role) {
+        const float* zr = zs_s + (rf * nq + i) * RCD;
+        const float* mr = m_s + (i % 3) * R * RCD + ((i + 1) * RCD + rk) * RCD;
+        float* pp = pu_s + (rf * nq + i + 1) * RCD + rk;
+        zn = *pp - dot8(ld4(mr), ld4(mr + 4), ld4(zr), ld4(zr + 4));
+        *pp = zn;
+      }
+      set_e(zn);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        av[t][0] = an[t][0];
+        av[t][1] = an[t][1];
+      }
+    }
+    CSTAMP(i, 6);
+    __syncthreads();  // ------------------------------------------------- next stage's e
+    CSTAMP(i, 7);
+  }
+  CSTAMP(nq, 2);
+
+  // ---- epilogue: outputs of every stage (LDS -> HBM)
+  for (int e = tid; e < nf * nq * RCD; e += CH_NT) {
+    // zst [b][i][t][k] and latents [b][i*8+k][t]
+    const int k = e & 7, fi = e >> 3;
+    const int i = fi / nf, f = fi - i * nf;
+    const int n = n0 + f, b = n / a.T, t = n - b * a.T;
+    a.zst[(((size_t)b * nq + i) * a.T + t) * RCD + k] = zs_s[(f * nq + i) * RCD + k];
+    a.latents[(((size_t)b * nq + i) * RCD + k) * a.T + t] = lat_s[(f * nq + i) * RCD + k];
+  }
+  for (int e = tid; e < nf * nq; e += CH_NT) {
+    const int i = e / nf, f = e - i * nf;
+    const int n = n0 + f, b = n / a.T, t = n - b * a.T;
+    const size_t o = ((size_t)b * nq + i) * a.T + t;
+    a.codes[o] = (int64_t)code_s[f * nq + i];
+    a.loss_pf[o] = loss_s[f * nq + i];
+    if (a.mask) {
+      const float s = a.imp ? (a.imp[n] * a.level) * (float)nq : INFINITY;
+      a.mask[o] = (s - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:55-61
+    }
+  }
+  CSTAMP(nq, 3);
+}
+
+// ------------------------------------------------------------------------------------------
+// Expansion on the matrix cores: z_q_is[b,i,c,t] = (W_out(i)[c,:] . zst[b,i,t,:]) + b_out(i)[c]
+// and z_q[b,c,t] = sum_i mask[b,i,t] * z_q_is[b,i,c,t] (stage order, from 0: the masked_sum
+// kernel's expression bit for bit). One wave = one (clip, 32-channel, 32-frame) tile over all
+// stages; per stage five v_mfma_f32_32x32x2_f32 with K = 10: k < 8 the out_proj weights x zst,
+// k = 8 the bias x 1, k = 9 zero -- the k-ordered fma chain from 0, i.e. dot8(W, zst) + bias
+// with the reference's roundings. The accumulator layout puts 32 consecutive frames of one
+// channel row in each half-wave, so every store instruction writes two 128-B row runs.
+struct ExpandArgs {
+  const float* zst;    // [B][nq][T][8]
+  int B, D, T, nq;
+  const float* w_out;  // [nq][D][8]
+  const float* b_out;  // [nq][D]
+  const float* imp;    // [B][T] or null
+  float level;
+  float* z_q_is;       // [B][nq][D][T] or null
+  float* z_q;          // [B][D][T]
+  float* mask;         // [B][nq][T] or null
+  int n_ct, n_tt;      // 32-channel tiles, 32-frame tiles
+};
+
+__global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  // workgroup = 4 consecutive channel tiles of one (clip, frame tile)
+  int bid = blockIdx.x;
+  const int ctg = bid % ((a.n_ct + 3) / 4);
+  bid /= (a.n_ct + 3) / 4;
+  const int tt = bid % a.n_tt;
+  const int b = bid / a.n_tt;
+  const int ct = ctg * 4 + wave;
+  if (ct >= a.n_ct) return;  // no barrier in this kernel
+  const int c0 = ct * 32, t0 = tt * 32;
+  const int col = lane & 31, h = lane >> 5;
+  const int t = t0 + col;
+  const bool tv = t < a.T;
+  const int tc = tv ? t : a.T - 1;
+  const int cr = min(c0 + col, a.D - 1);  // A-operand row of this lane (clamped: D % 32 tail)
+  const float s = (a.imp && tv) ? (a.imp[(size_t)b * a.T + t] * a.level) * (float)a.nq : INFINITY;
+  const float* zp = a.zst + ((size_t)b * a.nq * a.T + tc) * RCD;
+  const size_t zstride = (size_t)a.T * RCD;
+  const float* wp = a.w_out + (size_t)cr * RCD;
+  const size_t wstride = (size_t)a.D * RCD;
+  f32x16 zq;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) zq[r] = 0.0f;
+  // operands of stage i, software-pipelined one stage ahead (the wait for them never covers
+  // the previous stage's stores: vmcnt counts stores too)
+  float4 w0 = ld4(wp), w1 = ld4(wp + 4), z0 = ld4(zp), z1 = ld4(zp + 4);
+  float bb = a.b_out[cr];
+  for (int i = 0; i < a.nq; ++i) {
+    const float4 cw0 = w0, cw1 = w1, cz0 = z0, cz1 = z1;
+    const float cb = bb;
+    if (i + 1 < a.nq) {
+      w0 = ld4(wp + (i + 1) * wstride);
+      w1 = ld4(wp + (i + 1) * wstride + 4);
+      z0 = ld4(zp + (i + 1) * zstride);
+      z1 = ld4(zp + (i + 1) * zstride + 4);
+      bb = a.b_out[(size_t)(i + 1) * a.D + cr];
+    }
+    // lane (col, h) supplies k = 2 s + h of step s
+    const float wa[4] = {h ? cw0.y : cw0.x, h ? cw0.w : cw0.z, h ? cw1.y : cw1.x, h ? cw1.w : cw1.z};
+    const float zb[4] = {h ? cz0.y : cz0.x, h ? cz0.w : cz0.z, h ? cz1.y : cz1.x, h ? cz1.w : cz1.z};
+    f32x16 q;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) q[r] = 0.0f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
+    // k = 8: bias x 1 (lanes h = 0), k = 9: 0 x 0 (lanes h = 1)
+    q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cb, h ? 0.0f : 1.0f, q, 0, 0, 0);
+    const float m = (s - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
+    if (a.mask && ct == 0 && h == 0 && tv) a.mask[((size_t)b * a.nq + i) * a.T + t] = m;
+    if (a.z_q_is && tv) {
+      float* dst = a.z_q_is + (((size_t)b * a.nq + i) * a.D + c0 + 4 * h) * a.T + t;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2);
+        if (c0 + 4 * h + row < a.D) dst[(size_t)row * a.T] = q[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) zq[r] = zq[r] + q[r] * m;
+  }
+  if (tv) {
+    float* dst = a.z_q + ((size_t)b * a.D + c0 + 4 * h) * a.T + t;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2);
+      if (c0 + 4 * h + row < a.D) dst[(size_t)row * a.T] = zq[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+int launch_project(const float* z, int batch, int frames, int nq, const float* w_in_t,
+                   float* part, hipStream_t st) {
+  const long long nf = (long long)batch * frames;
+  VRVQ_CHECK_ARG(nf * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
+  const int n_tc = (frames + PJ_TC - 1) / PJ_TC;
+  const dim3 grid((unsigned)(batch * n_tc), PJ_SPLIT, (unsigned)((nq + 7) / 8));
+  hipLaunchKernelGGL(rvq_project_kernel, grid, dim3(PJ_NT), 0, st, z, frames, nq, n_tc, w_in_t,
+                     part, (int)nf);
+  return vrvq_launch_status();
+}
+
+unsigned long long* g_stamps = nullptr;  // diagnostic build: vrvq_debug_set_stamps
+
+template <int NM>
+int launch_chain_nm(const ChainArgs& a, hipStream_t st, long long nblk) {
+  const size_t lds = (size_t)ChainLds(a.nq, a.F, 256 * NM).total * sizeof(float);
+  if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_chain_kernel<NM>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(rvq_chain_kernel<NM>, dim3((unsigned)nblk), dim3(CH_NT), lds, st, a);
+  return vrvq_launch_status();
+}
+
+int launch_chain(const ChainArgs& a0, int ncode, hipStream_t st) {
+  ChainArgs a = a0;
+  a.stamps = g_stamps;
+  // frames per workgroup: one workgroup per CU (<= 256 in one round) with as few frames each
+  // as that allows, at most 16 (one MFMA column tile). The stage time is latency-bound and
+  // nearly independent of F (measured: F = 6 at two workgroups per CU was no faster).
+  const long long nf = (long long)a.B * a.T;
+  long long F = (nf + 255) / 256;
+  F = F < 1 ? 1 : (F > CH_FMAX ? CH_FMAX : F);
+  a.F = (int)F;
+  a.NF = (int)nf;
+  const long long nblk = (nf + F - 1) / F;
+  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
+  switch (ncode / 256) {
+    case 1: return launch_chain_nm<1>(a, st, nblk);
+    case 2: return launch_chain_nm<2>(a, st, nblk);
+    case 3: return launch_chain_nm<3>(a, st, nblk);
+    default: return launch_chain_nm<4>(a, st, nblk);
+  }
+}
+
+int launch_expand(const float* zst, int batch, int dim, int frames, int nq, const float* w_out,
+                  const float* b_out, const float* imp, float level, float* z_q_is, float* z_q,
+                  float* mask, hipStream_t st) {
+  ExpandArgs a{zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask};
+  a.n_ct = (dim + 31) / 32;
+  a.n_tt = (frames + 31) / 32;
+  const long long nblk = (long long)batch * a.n_tt * ((a.n_ct + 3) / 4);
+  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
+  hipLaunchKernelGGL(rvq_expand_kernel, dim3((unsigned)nblk), dim3(256), 0, st, a);
+  return vrvq_launch_status();
+}
+
+bool rvq_shape_ok(int dim, int cdim, int nq, int ncode) {
+  return dim == RD && cdim == RCD && nq <= CH_NQMAX && ncode > 0 && ncode % 256 == 0 &&
+         ncode <= 1024;
+}
+
+size_t part_floats(long long nf, int nq) { return (size_t)PJ_SPLIT * nf * nq * RCD; }
 
 }  // namespace
 
-unsigned long long* vrvq_g_stamps = nullptr;  // shared with rvq_fused.hip (common.h)
-
-// Diagnostic hook (stamped builds only): per-block per-stage s_memtime stamps of the codes kernel.
+#ifdef VRVQ_STAMPS
+// Diagnostic build only (not in include/vrvq.h): the chain kernel's stamp buffer.
 extern "C" int vrvq_debug_set_stamps(unsigned long long* buf) {
-  vrvq_g_stamps = buf;
+  g_stamps = buf;
   return 0;
 }
+#endif
 
-extern "C" int vrvq_rvq_codes(const float* z, int batch, int dim, int frames, int nq, int ncode,
-                              int cdim, const float* w_in_t, const float* b_in, const float* cb,
-                              const float* cbn, const float* c2, const float* w_out,
-                              const float* b_out, int64_t* codes, float* latents,
-                              float* loss_pf, float* zst, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(z && w_in_t && b_in && cb && cbn && c2 && w_out && b_out && codes && latents &&
-                 loss_pf && zst);
-  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0);
-  if (dim != RVQ_D || cdim != RVQ_CD || ncode <= 0 || ncode % RVQ_THREADS != 0 ||
-      ncode > 1024)
-    return VRVQ_ERR_UNSUPPORTED;
-  CodesArgs a{z, batch, frames, nq, ncode, w_in_t, b_in, cb, cbn, c2, w_out, b_out,
-              codes, latents, loss_pf, zst, vrvq_g_stamps};
-  // Frame groups per workgroup: aim at one workgroup per CU (256 CUs), at most 3 groups
-  // (768 threads, 3 waves/SIMD).
-  const long long nf = (long long)batch * frames;
-  int fg = (int)((nf + RVQ_FPG * 256 - 1) / (RVQ_FPG * 256));
-  fg = fg < 1 ? 1 : (fg > 3 ? 3 : fg);
-  static const int fg_env = [] {  // tuning override: VRVQ_RVQ_FG=1|2|3
-    const char* e = getenv("VRVQ_RVQ_FG");
-    return e ? atoi(e) : 0;
-  }();
-  if (fg_env >= 1 && fg_env <= 3) fg = fg_env;
-  const long long nblk = (nf + fg * RVQ_FPG - 1) / (fg * RVQ_FPG);
-  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
-  hipStream_t st = as_stream(stream);
-  const int nm = ncode / RVQ_THREADS;
-#define VRVQ_CODES_LAUNCH(FGV, NMV) \
-  hipLaunchKernelGGL((rvq_codes_kernel<FGV, NMV>), dim3((unsigned)nblk), dim3(RVQ_THREADS * FGV), 0, st, a)
-#define VRVQ_CODES_NM(FGV)                      \
-  switch (nm) {                                 \
-    case 1: VRVQ_CODES_LAUNCH(FGV, 1); break;   \
-    case 2: VRVQ_CODES_LAUNCH(FGV, 2); break;   \
-    case 3: VRVQ_CODES_LAUNCH(FGV, 3); break;   \
-    default: VRVQ_CODES_LAUNCH(FGV, 4); break;  \
-  }
-  if (fg == 1) { VRVQ_CODES_NM(1) }
-  else if (fg == 2) { VRVQ_CODES_NM(2) }
-  else { VRVQ_CODES_NM(3) }
-#undef VRVQ_CODES_NM
-#undef VRVQ_CODES_LAUNCH
+extern "C" int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_out,
+                                   int nq, int dim, int cdim, float* mcol, float* qb,
+                                   vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w_in_t && w_out && b_out && mcol && qb && nq > 0);
+  if (dim != RD || cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
+  const int total = nq * nq * 64 + nq * RCD;
+  hipLaunchKernelGGL(cross_prep_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     as_stream(stream), w_in_t, w_out, b_out, nq, mcol, qb);
   return vrvq_launch_status();
+}
+
+extern "C" int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
+                             vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(cbn && cbf && nq > 0);
+  if (!rvq_shape_ok(RD, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  const size_t total = (size_t)nq * ncode * RCD;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(rvq_frag_kernel, dim3(grid), dim3(256), 0, as_stream(stream), cbn, nq,
+                     ncode, cbf);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_rvq_project(const float* z, int batch, int dim, int frames, int nq, int cdim,
+                                const float* w_in_t, float* part, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(z && w_in_t && part && batch > 0 && frames > 0 && nq > 0);
+  if (dim != RD || cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
+  return launch_project(z, batch, frames, nq, w_in_t, part, as_stream(stream));
+}
+
+extern "C" int vrvq_rvq_chain(const float* part, int batch, int frames, int nq, int ncode,
+                              int cdim, const float* b_in, const float* qb, const float* mcol,
+                              const float* cb, const float* cbf, const float* c2,
+                              const float* imp, float level, int64_t* codes, float* latents,
+                              float* loss_pf, float* zst, float* mask, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(part && b_in && qb && mcol && cb && cbf && c2 && codes && latents && loss_pf &&
+                 zst);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0);
+  if (!rvq_shape_ok(RD, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  ChainArgs a{};
+  a.part = part; a.B = batch; a.T = frames; a.nq = nq;
+  a.b_in = b_in; a.qb = qb; a.mcol = mcol; a.cb = cb; a.cbf = cbf; a.c2 = c2;
+  a.imp = imp; a.level = level;
+  a.codes = codes; a.latents = latents; a.loss_pf = loss_pf; a.zst = zst; a.mask = mask;
+  return launch_chain(a, ncode, as_stream(stream));
 }
 
 extern "C" int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames, int nq, int cdim,
@@ -490,15 +765,43 @@ extern "C" int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames,
                                vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(zst && w_out && b_out && z_q);
   VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim > 0);
-  if (cdim != RVQ_CD || dim % EXP_CB != 0) return VRVQ_ERR_UNSUPPORTED;
-  ExpandArgs a{zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask,
-               dim / EXP_CB};
+  if (cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
+  return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask,
+                       as_stream(stream));
+}
+
+extern "C" int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0);
   const long long nf = (long long)batch * frames;
-  const long long nblk = (nf + EXP_THREADS - 1) / EXP_THREADS * a.n_cc;
-  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
-  const size_t lds = (size_t)nq * EXP_CB * (RVQ_CD + 1) * sizeof(float);
-  if (lds > 64 * 1024) return VRVQ_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(rvq_expand_kernel, dim3((unsigned)nblk), dim3(EXP_THREADS), lds,
-                     as_stream(stream), a, zst, w_out, b_out, imp, z_q_is, z_q, mask);
-  return vrvq_launch_status();
+  *bytes = (long long)(part_floats(nf, nq) + (size_t)nf * nq * RCD) * (long long)sizeof(float);
+  return 0;
+}
+
+extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, int nq, int ncode,
+                               int cdim, const float* w_in_t, const float* b_in, const float* cb,
+                               const float* cbf, const float* c2, const float* w_out,
+                               const float* b_out, const float* mcol, const float* qb,
+                               const float* imp, float level, int64_t* codes, float* latents,
+                               float* loss_pf, float* z_q_is, float* z_q, float* mask,
+                               void* workspace, long long workspace_bytes,
+                               vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(z && w_in_t && b_in && cb && cbf && c2 && w_out && b_out && mcol && qb &&
+                 codes && latents && loss_pf && z_q && workspace);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0);
+  if (!rvq_shape_ok(dim, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  long long need = 0;
+  vrvq_rvq_workspace(batch, frames, nq, &need);
+  VRVQ_CHECK_ARG(workspace_bytes >= need);
+  VRVQ_CHECK_ARG(((uintptr_t)workspace & 15) == 0);
+  const long long nf = (long long)batch * frames;
+  float* part = static_cast<float*>(workspace);
+  float* zst = part + part_floats(nf, nq);
+  hipStream_t st = as_stream(stream);
+  int rc = launch_project(z, batch, frames, nq, w_in_t, part, st);
+  if (rc) return rc;
+  rc = vrvq_rvq_chain(part, batch, frames, nq, ncode, cdim, b_in, qb, mcol, cb, cbf, c2, imp,
+                      level, codes, latents, loss_pf, zst, mask, stream);
+  if (rc) return rc;
+  return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q,
+                       nullptr, st);
 }

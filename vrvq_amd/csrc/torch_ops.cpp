@@ -262,7 +262,7 @@ void check_rvq_weights(const Tensor& z, const Tensor& w_in_t, const Tensor& b_in
   check_on(c2, z, "c2");
   check_on(w_out, z, "w_out");
   check_on(b_out, z, "b_out");
-  TORCH_CHECK(cb.dim() == 3 && cbn.sizes() == cb.sizes(), "rvq: cb / cbn must be (nq, N, d)");
+  TORCH_CHECK(cb.dim() == 3 && cbn.sizes() == cb.sizes(), "rvq: cb / cbf must be (nq, N, d)");
   const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2), D = z.size(1);
   TORCH_CHECK(c2.numel() == nq * N, "rvq: c2 must be (nq, N)");
   TORCH_CHECK(w_in_t.sizes() == at::IntArrayRef({nq, D, d}) &&
@@ -271,19 +271,56 @@ void check_rvq_weights(const Tensor& z, const Tensor& w_in_t, const Tensor& b_in
   TORCH_CHECK(b_in.numel() == nq * d && b_out.numel() == nq * D, "rvq: bias shapes");
 }
 
+// Cross terms of the projected chain (include/vrvq.h): once per weight version.
+std::tuple<Tensor, Tensor> rvq_cross_prep(const Tensor& w_in_t, const Tensor& w_out,
+                                          const Tensor& b_out) {
+  check_t(w_in_t, "w_in_t");
+  check_on(w_out, w_in_t, "w_out");
+  check_on(b_out, w_in_t, "b_out");
+  TORCH_CHECK(w_in_t.dim() == 3 && w_out.sizes() == w_in_t.sizes(),
+              "rvq_cross_prep: w_in_t / w_out must be (nq, D, d)");
+  c10::DeviceGuard guard(w_in_t.device());
+  const int64_t nq = w_in_t.size(0), D = w_in_t.size(1), d = w_in_t.size(2);
+  Tensor mcol = empty_f({nq, nq, d, d}, w_in_t);
+  Tensor qb = empty_f({nq, d}, w_in_t);
+  check_rc(vrvq_rvq_cross_prep(w_in_t.data_ptr<float>(), w_out.data_ptr<float>(),
+                               b_out.data_ptr<float>(), (int)nq, (int)D, (int)d,
+                               mcol.data_ptr<float>(), qb.data_ptr<float>(), stream_of(w_in_t)),
+           "vrvq_rvq_cross_prep");
+  return {mcol, qb};
+}
+
+// The normalised codebooks in the chain's MFMA fragment order (include/vrvq.h, vrvq_rvq_frag).
+Tensor rvq_frag(const Tensor& cbn) {
+  check_t(cbn, "cbn");
+  TORCH_CHECK(cbn.dim() == 3, "rvq_frag: cbn must be (nq, N, d)");
+  c10::DeviceGuard guard(cbn.device());
+  Tensor cbf = at::empty_like(cbn);
+  check_rc(vrvq_rvq_frag(cbn.data_ptr<float>(), (int)cbn.size(0), (int)cbn.size(1),
+                         (int)cbn.size(2), cbf.data_ptr<float>(), stream_of(cbn)),
+           "vrvq_rvq_frag");
+  return cbf;
+}
+
 // VBRResidualVectorQuantize.forward quantizer loop + gating (models/quantize.py:328-443) and
 // ResidualVectorQuantize.forward in eval (:136-214): all stages, z_q_is, mask, masked z_q.
+// The three launches' workspace comes from the caching allocator (stream-ordered reuse).
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode(
     const Tensor& z, const Tensor& w_in_t, const Tensor& b_in, const Tensor& cb,
-    const Tensor& cbn, const Tensor& c2, const Tensor& w_out, const Tensor& b_out,
-    const optional<Tensor>& imp, double level, bool want_z_q_is, bool want_mask) {
+    const Tensor& cbf, const Tensor& c2, const Tensor& w_out, const Tensor& b_out,
+    const Tensor& mcol, const Tensor& qb, const optional<Tensor>& imp, double level,
+    bool want_z_q_is, bool want_mask) {
   check_t(z, "z");
   TORCH_CHECK(z.dim() == 3, "rvq_encode: z must be (B, D, T)");
-  check_rvq_weights(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out);
+  check_rvq_weights(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out);
+  check_on(mcol, z, "mcol");
+  check_on(qb, z, "qb");
   check_opt(imp, z, "imp");
   c10::DeviceGuard guard(z.device());
   const int64_t B = z.size(0), D = z.size(1), T = z.size(2);
   const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2);
+  TORCH_CHECK(mcol.numel() == nq * nq * d * d && qb.numel() == nq * d,
+              "rvq_encode: cross terms (rvq_cross_prep) do not match nq");
   if (imp.has_value()) TORCH_CHECK(imp->numel() == B * T, "rvq_encode: imp must hold B*T values");
   Tensor codes = at::empty({B, nq, T}, z.options().dtype(at::kLong));
   Tensor latents = empty_f({B, nq * d, T}, z);
@@ -291,14 +328,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode(
   Tensor z_q_is = want_z_q_is ? empty_f({B, nq, D, T}, z) : none_like(z);
   Tensor z_q = empty_f({B, D, T}, z);
   Tensor mask = want_mask ? empty_f({B, nq, T}, z) : none_like(z);
-  check_rc(vrvq_rvq_fused(z.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)N, (int)d,
-                          w_in_t.data_ptr<float>(), b_in.data_ptr<float>(), cb.data_ptr<float>(),
-                          cbn.data_ptr<float>(), c2.data_ptr<float>(), w_out.data_ptr<float>(),
-                          b_out.data_ptr<float>(), fp(imp), (float)level,
-                          codes.data_ptr<int64_t>(), latents.data_ptr<float>(),
-                          loss_pf.data_ptr<float>(), opt_ptr(z_q_is), z_q.data_ptr<float>(),
-                          opt_ptr(mask), stream_of(z)),
-           "vrvq_rvq_fused");
+  long long ws_bytes = 0;
+  check_rc(vrvq_rvq_workspace((int)B, (int)T, (int)nq, &ws_bytes), "vrvq_rvq_workspace");
+  Tensor ws = at::empty({(ws_bytes + 3) / 4}, z.options().dtype(at::kFloat));
+  check_rc(vrvq_rvq_encode(z.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)N, (int)d,
+                           w_in_t.data_ptr<float>(), b_in.data_ptr<float>(), cb.data_ptr<float>(),
+                           cbf.data_ptr<float>(), c2.data_ptr<float>(), w_out.data_ptr<float>(),
+                           b_out.data_ptr<float>(), mcol.data_ptr<float>(), qb.data_ptr<float>(),
+                           fp(imp), (float)level, codes.data_ptr<int64_t>(),
+                           latents.data_ptr<float>(), loss_pf.data_ptr<float>(), opt_ptr(z_q_is),
+                           z_q.data_ptr<float>(), opt_ptr(mask), ws.data_ptr<float>(),
+                           (long long)ws.numel() * 4, stream_of(z)),
+           "vrvq_rvq_encode");
   return {codes, latents, loss_pf, z_q_is, z_q, mask};
 }
 
@@ -516,10 +557,12 @@ TORCH_LIBRARY(vrvq, m) {
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "
       "bool want_raw) -> (Tensor, Tensor)");
+  m.def("rvq_cross_prep(Tensor w_in_t, Tensor w_out, Tensor b_out) -> (Tensor, Tensor)");
+  m.def("rvq_frag(Tensor cbn) -> Tensor");
   m.def(
-      "rvq_encode(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbn, Tensor c2, "
-      "Tensor w_out, Tensor b_out, Tensor? imp, float level, bool want_z_q_is, bool want_mask) "
-      "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+      "rvq_encode(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
+      "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
+      "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("rvq_gather(Tensor codes, Tensor cb) -> (Tensor, Tensor, Tensor)");
   m.def(
       "rvq_expand(Tensor zst, Tensor w_out, Tensor b_out, Tensor? imp, float level, "
@@ -548,6 +591,8 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("snake_conv1d", &snake_conv1d); \
   m.impl("snake_conv_transpose1d", &snake_conv_transpose1d); \
   m.impl("residual_unit", &residual_unit); \
+  m.impl("rvq_cross_prep", &rvq_cross_prep); \
+  m.impl("rvq_frag", &rvq_frag); \
   m.impl("rvq_encode", &rvq_encode); \
   m.impl("rvq_gather", &rvq_gather); \
   m.impl("rvq_expand", &rvq_expand); \

@@ -140,16 +140,21 @@ class _Stacked:
         self.b_in = torch.stack(b_in).contiguous()
         self.cb = torch.stack(cb).contiguous()
         self.cbn, self.c2 = ops.codebook_prep(self.cb)
+        self.cbf = ops.rvq_frag(self.cbn)  # the chain's MFMA fragment order
         self.w_out = torch.stack(w_out).contiguous()
         self.b_out = torch.stack(b_out).contiguous()
+        # cross terms of the projected chain (include/vrvq.h, vrvq_rvq_cross_prep)
+        self.mcol, self.qb = ops.rvq_cross_prep(self.w_in_t, self.w_out, self.b_out)
 
     def codes_args(self):
-        return (self.w_in_t, self.b_in, self.cb, self.cbn, self.c2, self.w_out, self.b_out)
+        return (self.w_in_t, self.b_in, self.cb, self.cbf, self.c2, self.w_out, self.b_out,
+                self.mcol, self.qb)
 
     def prefix(self, n):
         s = _Stacked.__new__(_Stacked)
-        for k in ("w_in_t", "b_in", "cb", "cbn", "c2", "w_out", "b_out"):
+        for k in ("w_in_t", "b_in", "cb", "cbn", "cbf", "c2", "w_out", "b_out", "qb"):
             setattr(s, k, getattr(self, k)[:n].contiguous())
+        s.mcol = self.mcol[:n, :n].contiguous()
         return s
 
 

@@ -140,16 +140,28 @@ def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_p
 
 
 # ----------------------------------------------------------------------------- RVQ
-def rvq_encode(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp=None, level: float = 1.0,
-               want_z_q_is: bool = True, want_mask: bool = True):
+def rvq_cross_prep(w_in_t, w_out, b_out):
+    """M_ij = W_in[i] W_out[j] blocks (mcol [nq][nq][8][8]) and Qb [nq][8] of the projected
+    chain (once per weight version)."""
+    return _ops().rvq_cross_prep(w_in_t, w_out, b_out)
+
+
+def rvq_frag(cbn):
+    """The normalised codebooks in the chain's MFMA fragment order (once per weight version)."""
+    return _ops().rvq_frag(cbn)
+
+
+def rvq_encode(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
+               level: float = 1.0, want_z_q_is: bool = True, want_mask: bool = True):
     """The residual quantizer over all nq = cb.shape[0] stages + importance gating
-    (VBRResidualVectorQuantize.forward, models/quantize.py:328-443).
+    (VBRResidualVectorQuantize.forward, models/quantize.py:328-443): projection, 8-dim chain
+    and expansion (include/vrvq.h, vrvq_rvq_encode).
 
     Returns codes int64 [B,nq,T], latents [B,nq*d,T], loss_pf [B,nq,T], z_q_is [B,nq,D,T] (or
     None), z_q [B,D,T], mask [B,nq,T] (or None)."""
-    codes, lat, loss, zqis, zq, mask = _ops().rvq_encode(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out,
-                                                       imp, float(level), bool(want_z_q_is),
-                                                       bool(want_mask))
+    codes, lat, loss, zqis, zq, mask = _ops().rvq_encode(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out,
+                                                       mcol, qb, imp, float(level),
+                                                       bool(want_z_q_is), bool(want_mask))
     return codes, lat, loss, _none(zqis), zq, _none(mask)
 
 
@@ -248,8 +260,18 @@ def _register_fakes():
     def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw):
         return pair(x, tuple(x.shape), alpha_out, want_raw)
 
+    @reg("vrvq::rvq_cross_prep")
+    def _(w_in_t, w_out, b_out):
+        nq, _D, d = w_in_t.shape
+        return f32(w_in_t, (nq, nq, d, d)), f32(w_in_t, (nq, d))
+
+    @reg("vrvq::rvq_frag")
+    def _(cbn):
+        return torch.empty_like(cbn)
+
     @reg("vrvq::rvq_encode")
-    def _(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out, imp, level, want_z_q_is, want_mask):
+    def _(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp, level, want_z_q_is,
+          want_mask):
         B, D, T = z.shape
         nq, _n, d = cb.shape
         return (z.new_empty((B, nq, T), dtype=torch.int64), f32(z, (B, nq * d, T)),
