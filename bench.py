@@ -3,23 +3,29 @@
 (Snake/WNConv encoder + RVQ + importance gating) -> decode, batch 32 x 1 s @ 44.1 kHz per GPU
 (BASELINE.json configs[1]), synthetic audio resident in HBM, recipe (random-init) weights.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]                 configs[1] (default)
+    python bench.py --batch 64 --n-codebooks 32                      configs[2] shape
+    python bench.py --sweep [--batch 16]                             configs[4]: VBR level sweep
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank/GPU)
 
-Multi-GPU: clips shard data-parallel (each rank its own 32 clips, no data-path collective),
-weak scaling; the timed region is bracketed by barrier + synchronize and the MAX over ranks is
-reported. Rank 0 prints one JSON line, including
-  roofline      the single-launch RVQ kernel (vrvq_rvq_fused: residual chain + z_q_is stream +
-                importance gating) against HBM, bytes per SURVEY.md §8(d), per-launch
-                durations from HIP events recorded on the launch stream inside the timed steps;
+Multi-GPU: clips shard data-parallel (each rank its own clips, no data-path collective), weak
+scaling; the timed region is bracketed by barrier + synchronize and the MAX over ranks is
+reported; the sweep's [audio seconds, bits, frames] are SUM-reduced over ranks (RCCL) so its
+bpf / kbps are job-wide. Rank 0 prints one JSON line, including
+  roofline      the RVQ path (torch.ops.vrvq.rvq_encode: projection -> chain -> expansion)
+                against HBM, bytes per SURVEY.md §8(d), per-launch durations from HIP events
+                recorded on the launch stream inside the timed steps; per-kernel split from the
+                committed rocprofv3 summary; traffic from the committed PMC passes;
   roofline_conv the fp32-MFMA conv stacks against the fp32 matrix peak;
-  cpu_baseline  the CPU oracle (numpy, oracle/vrvq_oracle.py) timed on this host on a bounded
-                sample (rank 0, N=1 only).
+  cpu_baseline  oracle/torch_ref.py (a pure-PyTorch CPU restatement of the reference forward,
+                fixture-pinned) timed on this host on a bounded sample (rank 0, N=1 only).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
+import math
 import os
 import sys
 import time
@@ -35,10 +41,12 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (= vector peak)
 CLIP_SAMPLES = 44100
 SR = 44100
+LEVELS = (0.25, 0.5, 1.0, 2.0)
+RVQ_KERNELS = ("rvq_project_kernel", "rvq_chain_kernel", "rvq_expand_kernel")
 
 
 def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024) -> int:
-    """Algorithmic HBM bytes of one RVQ launch:
+    """Algorithmic HBM bytes of one RVQ pass:
     per frame z read, imp read, z_q_is + z_q writes, codes (int64), latents, mask, loss;
     plus the stage weights (normalised codebook counted once more)."""
     per_frame = D * 4 + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
@@ -46,132 +54,161 @@ def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024)
     return B * T * per_frame + weights
 
 
-def rvq_pmc_traffic(kernel: str = "rvq_fused_kernel<4>"):
-    """HBM bytes per launch of the RVQ kernel from the newest committed PMC measurement
-    (profiles/*_rvq_pmc.json: rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, made by
-    tools/gpu/pmc_rvq.sh at this workload). bench.py cannot collect PMC counters itself (they
-    need their own rocprofv3 passes), so it reports that measurement and names its file."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_rvq_pmc.json")))
-    if not files:
+def newest(pattern: str):
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    return files[-1] if files else None
+
+
+def rvq_pmc_traffic():
+    """HBM bytes per RVQ pass from the newest committed PMC measurement
+    (profiles/*_rvq_pmc.json: rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the three
+    kernels, separate passes, tools/gpu/pmc_rvq.sh at configs[1]). bench.py cannot collect PMC
+    counters itself (they need their own rocprofv3 passes), so it reports that file."""
+    f = newest("*_rvq_pmc.json")
+    if f is None:
         return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    return (int(k["total"]) if k else None), os.path.relpath(files[-1], REPO)
+    d = json.load(open(f))
+    return d.get("path_total_bytes"), os.path.relpath(f, REPO)
 
 
-def conv_flops(model, B: int, L: int) -> float:
-    """Algorithmic conv FLOPs of one encode+decode (2 * MACs over every conv layer), counted
-    from the layer geometry: the implicit GEMM's M x N x K per layer."""
-    from vrvq_amd.layers import WNConv1d, WNConvTranspose1d
+def rvq_kernel_split():
+    """Per-kernel average duration (us) of the RVQ launches from the newest committed
+    rocprofv3 kernel-stats summary (profiles/*_rvq_kernel_stats.csv)."""
+    import csv
+    f = newest("*_rvq_kernel_stats.csv")
+    if f is None:
+        return None, None
+    out = {}
+    for r in csv.DictReader(open(f)):
+        for k in RVQ_KERNELS:
+            if k in r["Name"]:
+                out[k] = round(float(r["AverageNs"]) / 1e3, 2)
+    return out, os.path.relpath(f, REPO)
 
-    flops = 0.0
-    T = L
-    # walk encoder / imp subnet / decoder in execution order with their time lengths
+
+def conv_flops(model, B: int, L: int):
+    """Algorithmic conv FLOPs (2 * MACs) of one encode (encoder + importance subnet) and one
+    decode, counted from the layer geometry: the implicit GEMM's M x N x K per layer."""
+    fl = {"enc": 0.0, "dec": 0.0}
+
     def conv_len(T, m):
         k, s, p, d = m.kernel_size[0], m.stride[0], m.padding[0], m.dilation[0]
         return (T + 2 * p - d * (k - 1) - 1) // s + 1
 
-    def acc_conv(m, Tin):
-        nonlocal flops
+    def acc(part, m, Tin):
         Tout = conv_len(Tin, m)
-        flops += 2.0 * B * m.out_channels * Tout * m.in_channels * m.kernel_size[0]
+        fl[part] += 2.0 * B * m.out_channels * Tout * m.in_channels * m.kernel_size[0]
         return Tout
 
     enc = model.encoder.block
-    T = acc_conv(enc[0], T)
+    T = acc("enc", enc[0], L)
     for i in range(1, len(enc) - 2):
         blk = enc[i].block
         for r in range(3):
-            acc_conv(blk[r].block[1], T)
-            acc_conv(blk[r].block[3], T)
-        T = acc_conv(blk[4], T)
-    T = acc_conv(enc[len(enc) - 1], T)
+            acc("enc", blk[r].block[1], T)
+            acc("enc", blk[r].block[3], T)
+        T = acc("enc", blk[4], T)
+    T = acc("enc", enc[len(enc) - 1], T)
     Tz = T
     if hasattr(model.quantizer, "imp_subnet"):
         sub = model.quantizer.imp_subnet
-        acc_conv(sub.in_block[1], Tz)
+        acc("enc", sub.in_block[1], Tz)
         for b in sub.blocks:
-            acc_conv(b[1], Tz)
+            acc("enc", b[1], Tz)
     dec = model.decoder.model
-    T = acc_conv(dec[0], Tz)
+    T = acc("dec", dec[0], Tz)
     for i in range(1, len(dec) - 3):
         blk = dec[i].block
         ct = blk[1]
-        flops += 2.0 * B * ct.in_channels * ct.out_channels * T * ct.kernel_size[0]
+        fl["dec"] += 2.0 * B * ct.in_channels * ct.out_channels * T * ct.kernel_size[0]
         T = T * ct.stride[0]
         for r in range(2, 5):
-            acc_conv(blk[r].block[1], T)
-            acc_conv(blk[r].block[3], T)
-    acc_conv(dec[len(dec) - 2], T)
-    return flops
+            acc("dec", blk[r].block[1], T)
+            acc("dec", blk[r].block[3], T)
+    acc("dec", dec[len(dec) - 2], T)
+    return fl["enc"], fl["dec"]
 
 
 class RvqTimer:
-    """HIP-event timing of the RVQ launch (vrvq_rvq_fused), recorded on the stream it runs
-    on."""
-
-    KERNELS = ("encode",)
+    """HIP-event timing of the RVQ operator (torch.ops.vrvq.rvq_encode: three launches),
+    recorded on the stream it runs on."""
 
     def __init__(self):
         self.events = []
         self.enabled = False
 
-    def mark(self, tag):
-        if self.enabled:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(torch.cuda.current_stream())
-            self.events.append((tag, e))
+    def install(self):
+        from vrvq_amd import ops
+        orig = ops.rvq_encode
 
-    def durations_ms(self):
-        torch.cuda.synchronize()
-        out = {k: [] for k in self.KERNELS}
-        ev = self.events
-        for (t0, e0), (t1, e1) in zip(ev, ev[1:]):
-            for k in self.KERNELS:
-                if t0 == k + "_begin" and t1 == k + "_end":
-                    out[k].append(e0.elapsed_time(e1))
-        return out
-
-
-def install_rvq_timer(timer: RvqTimer):
-    from vrvq_amd import ops
-
-    def wrap(name):
-        orig = getattr(ops, "rvq_" + name)
-
-        def f(*a, **k):
-            timer.mark(name + "_begin")
+        def timed(*a, **k):
+            if not self.enabled:
+                return orig(*a, **k)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream())
             r = orig(*a, **k)
-            timer.mark(name + "_end")
+            e1.record(torch.cuda.current_stream())
+            self.events.append((e0, e1))
             return r
-        setattr(ops, "rvq_" + name, f)
+        ops.rvq_encode = timed
 
-    for k in RvqTimer.KERNELS:
-        wrap(k)
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        v = [a.elapsed_time(b) for a, b in self.events]
+        return float(np.mean(v)) if v else float("nan")
 
 
-def cpu_baseline(kwargs, clips: int):
-    """The numpy CPU oracle on a bounded sample (same model/weights, `clips` x 1 s)."""
+def cpu_model() -> str:
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = os.cpu_count() or 1
-    from oracle.vrvq_oracle import Oracle
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(kwargs, clips: int, runs: int = 3):
+    """oracle/torch_ref.py (pure-PyTorch CPU restatement of the reference forward, pinned to the
+    reference's fixtures by tests/test_oracle.py) on a bounded sample of the same workload:
+    `clips` x 1 s clips, same recipe weights, 1 warm-up then the median of `runs`."""
+    from oracle.torch_ref import TorchRef
     from vrvq_amd.recipe import recipe_state_dict, synthetic_audio
     import vrvq_amd
 
-    shapes = {k: tuple(v.shape) for k, v in vrvq_amd.DAC_VRVQ(**kwargs).state_dict().items()}
-    o = Oracle(recipe_state_dict(shapes, 0), **kwargs)
-    audio = synthetic_audio(clips, CLIP_SAMPLES, seed=1234)
-    o.forward(audio[:1, :, :4096], None, 1.0)  # warm caches / BLAS threads
-    t0 = time.perf_counter()
-    o.forward(audio, None, 1.0)
-    dt = time.perf_counter() - t0
-    return {"value": clips * CLIP_SAMPLES / SR / dt, "unit": "audio-sec/s", "cores": int(threads),
-            "kind": "port",
-            "sample": f"{clips} x 1 s clip(s), full encode+RVQ+decode, numpy oracle, 1 run ({dt:.1f} s)"}
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        shapes = {k: tuple(v.shape) for k, v in vrvq_amd.DAC_VRVQ(**kwargs).state_dict().items()}
+        ref = TorchRef(recipe_state_dict(shapes, 0), **kwargs)
+        audio = torch.from_numpy(synthetic_audio(clips, CLIP_SAMPLES, seed=1234))
+        ref.forward(audio[:1], 1.0)  # warm-up (allocator, MKLDNN primitive caches, threads)
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            ref.forward(audio, 1.0)
+            ts.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    dt = float(np.median(ts))
+    return {"value": clips * CLIP_SAMPLES / SR / dt, "unit": "audio-sec/s", "cores": threads,
+            "kind": "port", "implementation": "torch-restatement (oracle/torch_ref.py)",
+            "cpu_model": cpu_model(), "median_of": runs,
+            "sample": f"{clips} x 1 s clips of the same workload (B={clips} of 32), full "
+                      f"preprocess+encode+RVQ+decode, torch CPU, 1 warm-up, median of {runs} "
+                      f"runs ({', '.join(f'{t:.2f}' for t in ts)} s)"}
+
+
+def build_model(args, dev):
+    import vrvq_amd
+    from vrvq_amd.recipe import load_recipe
+    kwargs = dict(encoder_dim=64, encoder_rates=[2, 4, 8, 8], decoder_dim=1536,
+                  decoder_rates=[8, 8, 4, 2], n_codebooks=args.n_codebooks, codebook_size=1024,
+                  codebook_dim=8, quantizer_dropout=1.0, sample_rate=SR)
+    model = vrvq_amd.DAC_VRVQ(**kwargs)
+    load_recipe(model, seed=0)
+    return model.to(dev).eval(), kwargs
 
 
 def main():
@@ -179,12 +216,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU (32; sweep 16)")
     ap.add_argument("--n-codebooks", type=int, default=8)
     ap.add_argument("--level", type=float, default=1.0)
-    ap.add_argument("--cpu-clips", type=int, default=16)
+    ap.add_argument("--sweep", action="store_true", help="configs[4]: VBR level sweep")
+    ap.add_argument("--cpu-clips", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 16 if args.sweep else 32
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -195,52 +235,84 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     import vrvq_amd
-    from vrvq_amd.recipe import load_recipe, synthetic_audio
-    from vrvq_amd.replicas import shard_seed, throughput, timed_steps
+    from vrvq_amd.recipe import synthetic_audio
+    from vrvq_amd.replicas import job_rate, shard_seed, throughput, timed_steps
 
-    kwargs = dict(encoder_dim=64, encoder_rates=[2, 4, 8, 8], decoder_dim=1536,
-                  decoder_rates=[8, 8, 4, 2], n_codebooks=args.n_codebooks, codebook_size=1024,
-                  codebook_dim=8, quantizer_dropout=1.0, sample_rate=SR)
-    model = vrvq_amd.DAC_VRVQ(**kwargs)
-    load_recipe(model, seed=0)
-    model = model.to(dev).eval()
-    audio = synthetic_audio(args.batch, CLIP_SAMPLES, seed=shard_seed(1234, rank))
-    audio = torch.from_numpy(audio).to(dev)
-
+    model, kwargs = build_model(args, dev)
+    audio = torch.from_numpy(synthetic_audio(args.batch, CLIP_SAMPLES,
+                                             seed=shard_seed(1234, rank))).to(dev)
     timer = RvqTimer()
-    install_rvq_timer(timer)
+    timer.install()
+    nq = args.n_codebooks
+    fps = math.floor(SR / model.hop_length)
+    lvl_ev = {lv: [] for lv in LEVELS}
 
-    def step():
-        with torch.no_grad():
-            return model(audio, SR, None, args.level)
+    if args.sweep:
+        # scripts/inference.py:88-112: encode once (level 1), then per level hard mask,
+        # masked sum of z_q_is, decode, bpf (device-side, no host sync inside the step)
+        bits = torch.full((nq,), 10.0, device=dev)
 
-    def timer_on():
+        def step():
+            with torch.no_grad():
+                enc = model.encode(model.preprocess(audio, SR), None, 1.0)
+                out = []
+                for lv in LEVELS:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    s = vrvq_amd.scale_importance(enc["imp_map"], lv * nq, 1.0)
+                    mask = vrvq_amd.generate_mask_hard(s, nq)
+                    y = model.decode(vrvq_amd.masked_sum(enc["z_q_is"], mask))
+                    bpf_t = vrvq_amd.ops.bpf(mask, bits)
+                    e1.record()
+                    if timer.enabled:
+                        lvl_ev[lv].append((e0, e1))
+                    out.append((lv, mask, bpf_t, y))
+                return out
+    else:
+        def step():
+            with torch.no_grad():
+                return model(audio, SR, None, args.level)
+
+    def on():
         timer.enabled = True
 
-    def timer_off():
+    def off():
         timer.enabled = False
 
     res_t = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize, device=dev,
-                        on_start=timer_on, on_stop=timer_off)
-    out = res_t.last
-    dt = res_t.seconds
-    ms_per_step = dt / args.steps * 1e3
+                        on_start=on, on_stop=off)
+    ms_per_step = res_t.seconds / args.steps * 1e3
     value = throughput(args.batch * CLIP_SAMPLES / SR, res_t)
-
-    durs = timer.durations_ms()
-    T = out["codes"].shape[-1]
-    byt = rvq_bytes(args.batch, T, args.n_codebooks)
-    per = {k: (float(np.mean(v)) if v else float("nan")) for k, v in durs.items()}
-    rvq_ms = sum(per.values())
+    T = math.ceil(CLIP_SAMPLES / model.hop_length)
+    rvq_ms = timer.mean_ms()
+    byt = rvq_bytes(args.batch, T, nq)
     achieved = byt / (rvq_ms * 1e-3) / 1e9
-    flops = conv_flops(model, args.batch, 44544)
-    # conv time per step = step time minus the RVQ launches (upper bound on conv kernel time)
+    fl_enc, fl_dec = conv_flops(model, args.batch, 44544)
+    flops = fl_enc + (len(LEVELS) if args.sweep else 1) * fl_dec
+    levels_rep = None
+    if args.sweep:
+        levels_rep = []
+        for lv, mask, bpf_t, _y in res_t.last:
+            rep = job_rate(args.batch * CLIP_SAMPLES / SR, float((mask.double() * 10.0).sum()),
+                           mask.shape[0] * mask.shape[2], fps, device=dev)
+            ms = float(np.mean([a.elapsed_time(b) for a, b in lvl_ev[lv]]))
+            levels_rep.append({"level": lv, "bpf": round(rep.bpf, 6), "kbps": round(rep.kbps, 4),
+                               "bpf_rank0_kernel": round(float(bpf_t), 6),
+                               "decode_ms_rank0": round(ms, 3),
+                               "decode_audio_sec_per_s": round(rep.audio_seconds /
+                                                               (ms * 1e-3), 2)})
     conv_ms = ms_per_step - rvq_ms
     conv_tflops = flops / (conv_ms * 1e-3) / 1e12
-
-    traffic, traffic_src = rvq_pmc_traffic() if (args.batch, args.n_codebooks) == (32, 8) \
-        else (None, None)
+    cfg2 = (args.batch, nq) == (32, 8) and not args.sweep
+    traffic, traffic_src = rvq_pmc_traffic() if cfg2 else (None, None)
+    split, split_src = rvq_kernel_split() if cfg2 else (None, None)
     if rank == 0:
+        workload = ("DAC_VRVQ conf/base.yml VBR, level sweep {0.25,0.5,1,2}: encode once + per "
+                    "level mask/masked-sum/decode/bpf (scripts/inference.py:88-112)"
+                    if args.sweep else
+                    f"DAC_VRVQ VBR {nq} cb, level {args.level}, preprocess+encode+decode "
+                    "(z_q_is materialised)")
         res = {
             "metric": "audio-sec/s encode+RVQ+decode, 44.1 kHz batch-32, 1->8 MI355X; RVQ HBM GB/s",
             "value": round(value, 3),
@@ -254,24 +326,26 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic uniform audio [-0.5,0.5), recipe random-init weights",
-            "config": {"workload": "DAC_VRVQ conf/base.yml VBR, level 1, preprocess+encode+decode "
-                                   "(z_q_is materialised)",
-                       "model": "DAC_VRVQ base (8 cb)", "global_batch": args.batch * world,
-                       "clip_samples": CLIP_SAMPLES, "n_codebooks": args.n_codebooks,
+            "config": {"workload": workload, "model": f"DAC_VRVQ base ({nq} cb)",
+                       "global_batch": args.batch * world, "clip_samples": CLIP_SAMPLES,
+                       "n_codebooks": nq,
                        "parallelism": f"dp{world} (replicas, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "rvq_fused_kernel (residual chain + z_q_is stream + gating)",
+                         "kernel": "RVQ path: rvq_project_kernel -> rvq_chain_kernel -> "
+                                   "rvq_expand_kernel (one torch.ops.vrvq.rvq_encode)",
                          "bytes_per_launch": byt, "path_us": round(rvq_ms * 1e3, 2),
-                         "launch_us": {k: round(v * 1e3, 2) for k, v in per.items()}},
+                         "kernel_us_rocprof": split, "kernel_us_source": split_src},
             "roofline_conv": {"bound": "mfma", "achieved": round(conv_tflops, 2),
                               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
                               "flops_per_step": flops,
                               "note": "algorithmic conv FLOPs / (step time - RVQ launches)"},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if levels_rep is not None:
+            res["levels"] = levels_rep
+        if world == 1 and not args.no_cpu_baseline and not args.sweep:
             res["cpu_baseline"] = cpu_baseline(kwargs, args.cpu_clips)
         print(json.dumps(res), flush=True)
     if world > 1:

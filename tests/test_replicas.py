@@ -9,7 +9,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from vrvq_amd.replicas import shard_range, shard_seed, throughput, timed_steps, TimedResult
+from vrvq_amd.replicas import (job_rate, shard_range, shard_seed, sum_over_ranks, throughput,
+                               timed_steps, TimedResult)
 
 
 def _free_port():
@@ -37,7 +38,18 @@ def _worker(rank, world, port, q):
         # every rank holds its own shard: gather the clip checksums
         sums = [None] * world
         dist.all_gather_object(sums, res.last)
-        q.put((rank, res.seconds, res.local_seconds, res.world, len(calls), sums))
+        # job-wide bpf from per-rank mask sums (SUM all-reduce) == bpf of the concatenated batch
+        import numpy as np
+        from oracle.vrvq_oracle import cal_bpf_from_mask, generate_mask_hard
+        rng = np.random.default_rng(7)
+        s_all = (rng.random((2 * world, 1, 11)) * 10).astype(np.float32)
+        mine = s_all[2 * rank: 2 * rank + 2]
+        mask = generate_mask_hard(mine, 8)
+        rep = job_rate(2.0, float((mask * 10).sum()), mask.shape[0] * mask.shape[2], 86)
+        want = cal_bpf_from_mask(generate_mask_hard(s_all, 8), [10] * 8)
+        tot = sum_over_ranks([rank + 1.0])
+        q.put((rank, res.seconds, res.local_seconds, res.world, len(calls), sums,
+               rep.bpf, want, rep.audio_seconds, rep.kbps, tot))
     finally:
         dist.destroy_process_group()
 
@@ -59,9 +71,12 @@ def test_timed_steps_two_ranks_gloo():
     t_max = maxes.pop()
     assert t_max == pytest.approx(max(g[2] for g in got))
     assert t_max >= 3 * 0.04                      # the slow rank's 3 timed steps
-    for rank, _, _, w, ncalls, sums in got:
+    for rank, _, _, w, ncalls, sums, bpf, want, audio_s, kbps, tot in got:
         assert w == world and ncalls == 5         # 2 warmup + exactly 3 timed
         assert sums[0] != sums[1]                 # distinct shards per rank
+        assert bpf == pytest.approx(want, rel=1e-12)
+        assert audio_s == 2.0 * world and kbps == pytest.approx(bpf * 86 / 1000)
+        assert tot == [3.0]
 
 
 def test_shard_range_partitions():

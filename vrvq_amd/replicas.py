@@ -3,8 +3,10 @@
 Clips are independent in the reference (`scripts/inference.py:88-112` loops over files; every
 op in `models/dac_vrvq.py:164-252` is per clip), so the path shards as replicas: each rank owns
 its own batch of clips and there is no collective on the data path. The only collectives are
-the ones that bracket a timed region: a barrier before and after, and an all_reduce(MAX) of the
-per-rank wall time, so the reported time is that of the slowest rank (weak scaling).
+reporting ones: a barrier before and after a timed region and an all_reduce(MAX) of the
+per-rank wall time, so the reported time is that of the slowest rank (weak scaling); and one
+all_reduce(SUM) of [audio seconds, bits, frames], so the job-wide bits per
+frame equals cal_bpf_from_mask (models/utils.py:64-73) over the concatenated batch.
 
 Backend-agnostic: `nccl` (RCCL over xGMI) on the GPU box, `gloo` in the CPU tests
 (tests/test_replicas.py, world_size 2).
@@ -53,6 +55,40 @@ def max_over_ranks(x: float, device: Optional[torch.device] = None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(values, device: Optional[torch.device] = None):
+    """all_reduce(SUM) of a per-rank list of floats in float64 (identity without a group)."""
+    vals = [float(v) for v in values]
+    if not _distributed() or dist.get_world_size() == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+@dataclass
+class RateReport:
+    """Job-wide totals of one level of the VBR sweep (scripts/inference.py:110-112)."""
+    audio_seconds: float
+    bits: float
+    frames: float
+    frames_per_second: int  # floor(sample_rate / hop_length)
+
+    @property
+    def bpf(self) -> float:
+        return self.bits / self.frames
+
+    @property
+    def kbps(self) -> float:
+        return self.bpf * self.frames_per_second / 1000
+
+
+def job_rate(audio_seconds: float, bits: float, frames: float, frames_per_second: int,
+             device: Optional[torch.device] = None) -> RateReport:
+    """Per-rank [audio_s, Σ mask·bits, B·T] -> job-wide RateReport (one SUM all-reduce)."""
+    a, b, f = sum_over_ranks([audio_seconds, bits, frames], device)
+    return RateReport(a, b, f, int(frames_per_second))
 
 
 def timed_steps(step: Callable[[], object], steps: int, warmup: int,
