@@ -266,6 +266,93 @@ int vrvq_unpack_codes(const uint16_t* packed, const int* counts, const long long
                       int batch, int nq, int frames, int64_t* codes, float* mask,
                       vrvq_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Training step (scripts/train.py:262-330): the backward operators of
+ * the generator, used by the torch.autograd.Functions in vrvq_amd/train.py. Every reduction
+ * runs in a fixed order (bitwise reproducible run to run).
+ * ------------------------------------------------------------------------------------- */
+
+/* Split-K plan for vrvq_conv1d_wgrad: *n_split partial sums and the workspace they need. */
+int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_split,
+                    long long* workspace_bytes);
+
+/* Weight gradient of a (Snake-fused) convolution as a split-K MFMA GEMM:
+ *   out[m][c][k] = sum_b sum_{t < ta} As[b][m][t] * Xs[b][c][t*stride - pad + k*dil]
+ * As = snake(a) if alpha_a, Xs = snake(x) if alpha (x = 0 outside [0, tx)).
+ *   WNConv1d (models/layers.py:17-18):      a = dY [B][Cout][Tout], x = layer input -> dW[Cout][Cin][k]
+ *   WNConvTranspose1d (models/layers.py:21-22): a = layer input (snake on a), x = dY
+ *                                           -> dW[Cin][Cout][k]
+ * The autograd conv weight backward of the reference (torch.nn.grad.conv1d_weight). */
+int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta, const float* alpha_a,
+                      const float* inv_alpha_a, const float* x, int c, int tx, const float* alpha,
+                      const float* inv_alpha, int k, int stride, int pad, int dil, int n_split,
+                      float* workspace, long long workspace_bytes, float* out,
+                      vrvq_stream_t stream);
+
+/* Snake1d backward (models/layers.py:26-32): dx = g (1 + inv sin(2 a x) a) (dx may be NULL),
+ * dalpha[c] = sum_{b,t} g (-inv^2 sin^2(a x) + inv sin(2 a x) x) (dalpha may be NULL). */
+int vrvq_snake_backward_workspace(int batch, int channels, int frames, long long* bytes);
+int vrvq_snake_backward(const float* x, const float* alpha, const float* inv_alpha,
+                        const float* grad, int batch, int channels, int frames, float* dx,
+                        float* dalpha, float* workspace, long long workspace_bytes,
+                        vrvq_stream_t stream);
+
+/* Conv bias gradient: db[c] = sum_{b,t} grad[b][c][t]. */
+int vrvq_bias_grad(const float* grad, int batch, int channels, int frames, float* db,
+                   vrvq_stream_t stream);
+
+/* Tanh (models/dac_vrvq.py:74) / Sigmoid (models/importance_subnet.py:44) backward from the
+ * saved output y: out = g (1 - y^2) | g y (1 - y). */
+int vrvq_act_backward(const float* y, const float* grad, long long n, int epilogue, float* out,
+                      vrvq_stream_t stream);
+
+/* weight_norm backward (models/layers.py:17-22): per row, n = ||v||,
+ * dg = (dw . v) / n, dv = (g / n) (dw - v (dw . v) / n^2). */
+int vrvq_weight_norm_backward(const float* g, const float* v, const float* dw, int rows,
+                              int cols, float* dg, float* dv, vrvq_stream_t stream);
+
+/* Adjoint packing for the input gradient of a stride-1 Conv1d: w [cout][cin][k] ->
+ * the vrvq_conv1d packed layout of W'[ci][co][k] = w[co][ci][k-1-k'] ([cout][k][cin_pad]). */
+int vrvq_pack_conv1d_flip(const float* w, int cout, int cin, int k, int cin_pad,
+                          float* w_packed, vrvq_stream_t stream);
+
+/* Training-mode importance mask (models/quantize.py:377-414, models/utils.py:11-61): rows
+ * b < n_imps: generate_mask_ste((imp * levels[b]) * nq, alpha) (value smooth + (hard - smooth));
+ * the next n_drop rows n_imps + j: generate_mask_hard(dropout[j]) (the first n_drop draws, as
+ * models/quantize.py:412-413 assigns dropout[:n_dropout]); the rest 1. imp [B][T], levels [B],
+ * dropout [B] int64 (may be NULL when n_drop = 0), mask [B][nq][T]. */
+int vrvq_mask_ste(const float* imp, const float* levels, const int64_t* dropout, int batch,
+                  int frames, int nq, float alpha, int n_imps, int n_drop, float* mask,
+                  vrvq_stream_t stream);
+/* Its backward: dimp[b][t] = (sum_i dmask[b][i][t] logcosh'(x - i)) * nq * levels[b] for
+ * b < n_imps, 0 for the overwritten rows. */
+int vrvq_mask_ste_backward(const float* imp, const float* levels, const float* dmask, int batch,
+                           int frames, int nq, float alpha, int n_imps, float* dimp,
+                           vrvq_stream_t stream);
+
+/* vrvq_rvq_expand with explicit mask values [B][nq][T] (the training mask) instead of imp. */
+int vrvq_rvq_expand_masked(const float* zst, int batch, int dim, int frames, int nq, int cdim,
+                           const float* w_out, const float* b_out, const float* mask,
+                           float* z_q_is, float* z_q, vrvq_stream_t stream);
+
+/* Backward of the training-mode quantizer (models/quantize.py:42-79, 328-443): from
+ * dz_q [B][D][T] and the device scalars g_commit / g_codebook (dL/d commitment_loss,
+ * dL/d codebook_loss) and the forward state (z, zst [B][nq][T][d], latents [B][nq*d][T], codes,
+ * mask values [B][nq][T]) computes dz [B][D][T], dmask [B][nq][T], dw_in [nq][d][D]
+ * (the folded in_proj weight layout), db_in [nq][d], dw_out [nq][D][d], db_out [nq][D] and
+ * dcb [nq][N][d]. D = 1024, d = 8, nq <= 32. The math (rvq_train.hip header) stays in the
+ * 8-dim latent space: reverse chain with M_ji = W_in(j) W_out(i) (mcol of
+ * vrvq_rvq_cross_prep), three split-K GEMMs and 8x8 fix-ups for the weight gradients. */
+int vrvq_rvq_backward_workspace(int batch, int frames, int nq, long long* bytes);
+int vrvq_rvq_backward(const float* dz_q, const float* g_commit, const float* g_codebook,
+                      const float* z, const float* zst, const float* latents,
+                      const int64_t* codes, const float* mask, int batch, int dim, int frames,
+                      int nq, int ncode, int cdim, const float* w_in_t, const float* w_out,
+                      const float* b_out, const float* mcol, const float* cb, float* dz,
+                      float* dmask, float* dw_in, float* db_in, float* dw_out, float* db_out,
+                      float* dcb, void* workspace, long long workspace_bytes,
+                      vrvq_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -256,10 +256,88 @@ def dac_file_fixture(ref_root):
     print("dac file", path)
 
 
+TRAIN_SAMPLES = 256   # gradient elements kept per parameter tensor (evenly spaced)
+TRAIN_FULL = 4096     # parameter tensors up to this size keep their whole gradient
+TRAIN_LAMBDAS = {"waveform": 1.0, "commitment": 0.25, "codebook": 1.0, "rate": 2.0}
+
+
+def grad_sample_index(numel):
+    return np.unique(np.linspace(0, numel - 1, min(numel, TRAIN_SAMPLES)).round().astype(np.int64))
+
+
+def train_fixture(DAC, kw, name, manifest, batch, seed, length=16758, audio_seed=4321):
+    """Generator gradients of one training step (scripts/train.py:262-330) under the reference's
+    own autograd: model.train(), the training-mode quantizer (random levels, dropout and
+    full-codebook rows drawn from torch's global CPU generator after torch.manual_seed(seed)),
+    and a surrogate generator loss with the vrvq_a2 weights of the terms that reach the
+    generator without a discriminator:
+        L = mean|audio - x| + 0.25 commitment + 1.0 codebook + 2.0 mean(imp_map)
+    (plain L1 in place of the audiotools L1Loss; mel/STFT/GAN terms are out of the fixture).
+    The components are called in DAC_VRVQ.forward's order (models/dac_vrvq.py:222-252) so the
+    intermediate gradients (z_q, z, feat) can be retained."""
+    model = build(DAC, kw)
+    model.train()
+    audio = synthetic_audio(batch, length, seed=audio_seed)
+    x = torch.from_numpy(audio)
+    nq = model.n_codebooks
+    torch.manual_seed(seed)
+    draws_levels = torch.rand((batch, 1, 1))
+    draws_dropout = torch.randint(1, nq + 1, (batch, 1, 1))
+    torch.manual_seed(seed)
+    xp = model.preprocess(x, 44100)
+    z, feat = model.encoder(xp, return_feat=True)
+    z.retain_grad()
+    feat.retain_grad()
+    enc = model.quantizer(z, None, feat, 1)
+    zq = enc["z_q"]
+    zq.retain_grad()
+    y = model.decode(zq)[..., :length]
+    lam = TRAIN_LAMBDAS
+    terms = {"waveform": (y - x).abs().mean(), "commitment": enc["commitment_loss"],
+             "codebook": enc["codebook_loss"], "rate": enc["imp_map"].mean()}
+    loss = sum(lam[k] * v for k, v in terms.items())
+    loss.backward()
+    res = {"audio_in": audio, "audio_out": y.detach().numpy(), "codes": enc["codes"].numpy(),
+           "mask_imp": enc["mask_imp"].detach().numpy(),
+           "imp_map": enc["imp_map"].detach().numpy(), "loss": np.float64(loss.item()),
+           "draws_levels": draws_levels.numpy(), "draws_dropout": draws_dropout.numpy(),
+           "grad_z_q": zq.grad.numpy(), "grad_z": z.grad.numpy(), "grad_feat": feat.grad.numpy()}
+    for k, v in terms.items():
+        res["term_" + k] = np.float64(v.item())
+    norms, params = {}, []
+    for pname, p in model.named_parameters():
+        g = p.grad.detach().reshape(-1).double()
+        norms[pname] = float(g.norm())
+        params.append(pname)
+        if g.numel() <= TRAIN_FULL:
+            res["g_full/" + pname] = g.float().numpy()
+        else:
+            res["g_s/" + pname] = g[torch.from_numpy(grad_sample_index(g.numel()))].float().numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+    n_full = int(batch * model.quantizer.full_codebook_rate)
+    n_drop = int(batch * model.quantizer.quantizer_dropout)
+    manifest[name] = {"kwargs": kw, "batch": batch, "length": length, "audio_seed": audio_seed,
+                      "weight_seed": 0, "rng_seed": seed, "lambdas": lam,
+                      "rows": {"imp": batch - n_full - n_drop, "dropout": n_drop, "full": n_full},
+                      "grad_norms": norms, "params": params,
+                      "sample_rule": f"linspace(0, numel-1, min(numel, {TRAIN_SAMPLES})) rounded, "
+                                     f"unique; tensors <= {TRAIN_FULL} elements kept whole"}
+    print(name, "loss", loss.item(), {k: float(v) for k, v in terms.items()},
+          "rows", manifest[name]["rows"])
+
+
+def train_all(DAC, ref, manifest):
+    a2 = yml_kwargs(ref, "conf/vrvq/vrvq_a2.yml")
+    train_fixture(DAC, a2, "golden_train_a2", manifest, batch=2, seed=2024)
+    # all three row kinds of the training quantizer (importance / dropout / full codebook)
+    train_fixture(DAC, dict(a2, quantizer_dropout=0.25), "golden_train_a2_rows", manifest,
+                  batch=4, seed=77)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.environ.get("VRVQ_REFERENCE", "/root/reference"))
-    ap.add_argument("--only", choices=["from_codes", "dac_file"], default=None,
+    ap.add_argument("--only", choices=["from_codes", "dac_file", "train"], default=None,
                     help="regenerate only these fixtures and merge them into manifest.json")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
@@ -267,10 +345,10 @@ def main():
     if args.only == "dac_file":
         dac_file_fixture(args.ref)
         return
-    if args.only == "from_codes":
+    if args.only in ("from_codes", "train"):
         with open(os.path.join(HERE, "manifest.json")) as f:
             manifest = json.load(f)
-        from_codes_all(DAC, args.ref, manifest)
+        (from_codes_all if args.only == "from_codes" else train_all)(DAC, args.ref, manifest)
         with open(os.path.join(HERE, "manifest.json"), "w") as f:
             json.dump(manifest, f, indent=1, default=float)
         return
@@ -293,6 +371,7 @@ def main():
     rvq_stress_fixture(DAC, k32, "golden_rvq_stress_nq32", manifest, batch=2, frames=40, seed=11)
     mask_kat(ref_utils, manifest)
     from_codes_all(DAC, args.ref, manifest)
+    train_all(DAC, args.ref, manifest)
     dac_file_fixture(args.ref)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, default=float)

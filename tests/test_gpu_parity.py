@@ -421,7 +421,8 @@ def _random_rvq(nq, ncode, seed):
 @pytest.mark.parametrize("nq,ncode,B,T,vbr", [
     (8, 1024, 3, 87, True), (8, 1024, 2, 1, True), (8, 1024, 2, 13, True), (8, 1024, 1, 25, False),
     (1, 1024, 4, 87, False), (32, 1024, 2, 87, True), (4, 256, 3, 40, True), (4, 512, 2, 87, True),
-    (4, 768, 2, 12, False), (28, 1024, 2, 70, True), (8, 1024, 5, 200, True)])
+    (4, 768, 2, 12, False), (28, 1024, 2, 70, True), (8, 1024, 5, 200, True),
+    (9, 1024, 2, 87, True), (5, 1024, 3, 40, False), (1, 1024, 3, 50, True)])
 def test_rvq_encode_vs_fp64(nq, ncode, B, T, vbr):
     """torch.ops.vrvq.rvq_encode against a torch fp64 reference: every codebook size variant
     (N/256 = 1..4), partial and exact frame ranges, nq = 1 .. 32, VBR and CBR; z_q_is also

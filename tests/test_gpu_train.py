@@ -1,0 +1,305 @@
+"""Training step on the MI355X: generator gradients of the HIP autograd
+path (vrvq_amd/train.py) against
+
+  - fixtures from the reference's own autograd (tests/golden/make_golden.py train_fixture:
+    vrvq_a2, 28 codebooks, 0.38 s clips, seeded training-mode quantizer, surrogate loss
+    L = mean|audio - x| + 0.25 commitment + codebook + 2 mean(imp_map));
+  - torch fp64 autograd restatements of each backward operator (conv / ConvT / Snake / weight
+    norm / activations, the mask STE and the quantizer with the straight-through estimator).
+
+Bar: seed-controlled draws bit-exact, codes bit-exact, every gradient tensor within 1e-4
+relative (L2 norm of the difference over the L2 norm of the reference, per tensor)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import vrvq_amd
+from conftest import load_golden, rel_err
+from vrvq_amd import ops, train
+from vrvq_amd.recipe import load_recipe
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+DEV = torch.device("cuda:0")
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def l2rel(a, b):
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# ------------------------------------------------------------------ torch fp64 references
+def snake64(x, alpha):
+    return x + (alpha + 1e-9).reciprocal() * torch.sin(alpha * x).pow(2)
+
+
+def wn64(g, v):
+    return torch._weight_norm(v, g, 0)
+
+
+CONV_CASES = [
+    # kind, cin, cout, k, stride, pad, dil, snake, residual, epi, T
+    ("conv", 64, 64, 7, 1, 9, 3, True, False, 0, 300),
+    ("conv", 96, 96, 1, 1, 0, 1, True, True, 0, 257),
+    ("conv", 1, 64, 7, 1, 3, 1, False, False, 0, 400),
+    ("conv", 64, 128, 4, 2, 1, 1, True, False, 0, 256),
+    ("conv", 128, 256, 16, 8, 4, 1, True, False, 0, 512),
+    ("conv", 512, 1, 3, 1, 1, 1, True, False, 2, 40),
+    ("conv", 96, 1, 7, 1, 3, 1, True, False, 1, 333),
+    ("convt", 256, 128, 16, 8, 4, 1, True, False, 0, 40),
+    ("convt", 192, 96, 4, 2, 1, 1, True, False, 0, 100),
+    ("convt", 384, 192, 8, 4, 2, 1, True, False, 0, 64),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "-".join(map(str, c)))
+def test_snake_conv_grads_vs_torch64(case):
+    kind, cin, cout, k, s, p, d, use_snake, use_res, epi, T = case
+    g0 = torch.Generator().manual_seed(17)
+    B = 2
+    x = torch.randn(B, cin, T, generator=g0)
+    alpha = torch.rand(cin, generator=g0) + 0.5
+    if kind == "conv":
+        v = torch.randn(cout, cin, k, generator=g0) * 0.1
+        g = torch.rand(cout, generator=g0) + 0.5
+    else:
+        v = torch.randn(cin, cout, k, generator=g0) * 0.1
+        g = torch.rand(cin, generator=g0) + 0.5
+    bias = torch.randn(cout, generator=g0) * 0.1
+
+    def ref(x, alpha, g, v, bias, res):
+        xs = snake64(x, alpha[None, :, None]) if use_snake else x
+        w = wn64(g.reshape(-1, 1, 1), v)
+        if kind == "conv":
+            y = F.conv1d(xs, w, bias, s, p, d)
+        else:
+            y = F.conv_transpose1d(xs, w, bias, stride=s, padding=p)
+        if res is not None:
+            y = y + res
+        return torch.tanh(y) if epi == 1 else (torch.sigmoid(y) if epi == 2 else y)
+
+    leaves64 = [a.double().requires_grad_() for a in (x, alpha, g, v, bias)]
+    with torch.no_grad():
+        tout = ref(*[a.double() for a in (x, alpha, g, v, bias)], None).shape[-1]
+    res = torch.randn(B, cout, tout, generator=g0) if use_res else None
+    res64 = res.double().requires_grad_() if use_res else None
+    y64 = ref(*leaves64, res64)
+    gy = torch.randn(y64.shape, generator=g0)
+    y64.backward(gy.double())
+
+    leaves = [a.to(DEV).requires_grad_() for a in (x, alpha, g, v, bias)]
+    resd = res.to(DEV).requires_grad_() if use_res else None
+    spec = (kind, cout, k, s, p, d, epi)
+    y = train._SnakeConv.apply(leaves[0], leaves[1] if use_snake else None, leaves[2], leaves[3],
+                               leaves[4], resd, spec)
+    assert rel_err(y.detach().cpu().numpy(), y64.detach().numpy()) < TOL
+    y.backward(gy.to(DEV))
+    names = ["dx", "dalpha", "dg", "dv", "dbias"]
+    for nm, a, r in zip(names, leaves, leaves64):
+        if nm == "dalpha" and not use_snake:
+            continue
+        e = l2rel(a.grad.cpu().numpy(), r.grad.numpy())
+        assert e < TOL, f"{nm}: rel {e}"
+    if use_res:
+        assert l2rel(resd.grad.cpu().numpy(), res64.grad.numpy()) < TOL
+
+
+def test_wgrad_deterministic():
+    g0 = torch.Generator().manual_seed(3)
+    a = torch.randn(3, 96, 700, generator=g0).to(DEV)
+    x = torch.randn(3, 64, 700, generator=g0).to(DEV)
+    r1 = ops.conv1d_wgrad(a, x, 7, 1, 9, 3)
+    r2 = ops.conv1d_wgrad(a, x, 7, 1, 9, 3)
+    assert torch.equal(r1, r2)
+    ref = torch.nn.grad.conv1d_weight(x.double().cpu(), (96, 64, 7), a.double().cpu(), 1, 9, 3)
+    assert l2rel(r1.cpu().numpy(), ref.numpy()) < TOL
+
+
+# ------------------------------------------------------------------ mask STE
+def logcosh64(alpha, pmk):  # models/utils.py:11-32 restated
+    EPS = 1e-10
+    mask1 = pmk >= 0
+    pmk1 = pmk * mask1.detach()
+    ms1 = (torch.log(math.exp(alpha) + torch.exp(-2 * pmk1 * alpha) + EPS)
+           - torch.log(torch.exp(alpha * (-2 * pmk1 + 1)) + 1 + EPS)) / (2 * alpha) + 0.5
+    mask2 = pmk < 0
+    pmk2 = pmk * mask2.detach()
+    ms2 = (torch.log(torch.exp(alpha * (2 * pmk2 + 1)) + 1 + EPS)
+           - torch.log(math.exp(alpha) + torch.exp(alpha * 2 * pmk2) + EPS)) / (2 * alpha) + 0.5
+    return ms1 * mask1 + ms2 * mask2
+
+
+def test_mask_ste_vs_torch64():
+    B, T, nq, alpha = 5, 77, 28, 2.0
+    g0 = torch.Generator().manual_seed(9)
+    imp = torch.rand(B, 1, T, generator=g0)
+    levels = torch.rand(B, generator=g0) * 5.875 + 0.125
+    dropout = torch.randint(1, nq + 1, (B,), generator=g0)
+    n_imps, n_drop = 3, 1
+    imp64 = imp.double().requires_grad_()
+    x = imp64 * levels.double()[:, None, None] * nq
+    pm = x - torch.arange(nq, dtype=torch.float64)[None, :, None]
+    sm = logcosh64(alpha, pm)
+    q = (pm >= 0).double()
+    m64 = sm + (q - sm).detach()
+    m64 = m64.clone()
+    m64[n_imps:n_imps + n_drop] = ((dropout[:n_drop].double()[:, None, None]
+                                    - torch.arange(nq, dtype=torch.float64)[None, :, None]) >= 0).double()
+    m64[n_imps + n_drop:] = 1.0
+    gm = torch.randn(B, nq, T, generator=g0)
+    (m64 * gm.double()).sum().backward()
+    impd = imp.to(DEV).requires_grad_()
+    m = train._MaskSte.apply(impd, levels.to(DEV), dropout.to(DEV), nq, alpha, n_imps, n_drop)
+    np.testing.assert_allclose(m.detach().cpu().numpy(), m64.detach().numpy(), atol=1e-6)
+    (m * gm.to(DEV)).sum().backward()
+    assert l2rel(impd.grad.cpu().numpy(), imp64.grad.numpy()) < TOL
+
+
+# ------------------------------------------------------------------ quantizer backward
+def rvq64(z, mask, g_in, v_in, b_in, g_out, v_out, b_out, cb, codes):
+    """The reference quantizer loop (models/quantize.py:42-79, 353-423) in fp64 autograd with the
+    given codes (argmin decisions fixed: the straight-through estimator only uses them as
+    indices)."""
+    nq, N, d = cb.shape
+    D = z.shape[1]
+    w_in = wn64(g_in.reshape(-1, 1), v_in).reshape(nq, d, D)
+    w_out = wn64(g_out.reshape(-1, 1), v_out).reshape(nq, D, d)
+    residual = z
+    z_q = 0
+    commit = 0
+    cbl = 0
+    for i in range(nq):
+        z_e = torch.einsum("kc,bct->bkt", w_in[i], residual) + b_in[i][None, :, None]
+        zq = cb[i][codes[:, i]].permute(0, 2, 1)                       # (B, d, T)
+        commit_i = (z_e - zq.detach()).pow(2).mean(1)
+        cbl_i = (zq - z_e.detach()).pow(2).mean(1)
+        zst = z_e + (zq - z_e).detach()
+        z_q_i = torch.einsum("cm,bmt->bct", w_out[i], zst) + b_out[i][None, :, None]
+        residual = residual - z_q_i
+        z_q = z_q + z_q_i * mask[:, i][:, None, :]
+        commit = commit + commit_i * mask[:, i].detach()
+        cbl = cbl + cbl_i * mask[:, i].detach()
+    return z_q, commit.mean(), cbl.mean()
+
+
+@pytest.mark.parametrize("nq,B,T", [(4, 2, 20), (28, 2, 33), (9, 3, 70)])
+def test_rvq_backward_vs_torch64(nq, B, T):
+    D, d, N = 1024, 8, 1024
+    g0 = torch.Generator().manual_seed(nq * 100 + T)
+    z = torch.randn(B, D, T, generator=g0) * 0.5
+    g_in = torch.rand(nq * d, generator=g0) + 0.5
+    v_in = torch.randn(nq * d, D, generator=g0) * 0.03
+    b_in = torch.randn(nq, d, generator=g0) * 0.1
+    g_out = torch.rand(nq * D, generator=g0) + 0.5
+    v_out = torch.randn(nq * D, d, generator=g0) * 0.3
+    b_out = torch.randn(nq, D, generator=g0) * 0.1
+    cb = torch.randn(nq, N, d, generator=g0)
+    mask = (torch.rand(B, nq, T, generator=g0) < 0.7).float()
+    mask[:, 0] = 1.0
+    leaves = [a.to(DEV).requires_grad_() for a in (z, mask, g_in, v_in, b_in, g_out, v_out, b_out, cb)]
+    z_q, commit, cbl, codes, lat = train._RvqTrain.apply(*leaves)
+    leaves64 = [a.double().requires_grad_() for a in (z, mask, g_in, v_in, b_in, g_out, v_out, b_out, cb)]
+    zq64, c64, cb64 = rvq64(*leaves64, codes.cpu())
+    assert rel_err(z_q.detach().cpu().numpy(), zq64.detach().numpy()) < TOL
+    assert float(commit) == pytest.approx(float(c64), rel=TOL)
+    gz = torch.randn(B, D, T, generator=g0)
+    lc, lcb = 0.25, 1.0
+    (zq64 * gz.double()).sum().add(lc * c64 + lcb * cb64).backward()
+    ((z_q * gz.to(DEV)).sum() + lc * commit + lcb * cbl).backward()
+    names = ["dz", "dmask", "dg_in", "dv_in", "db_in", "dg_out", "dv_out", "db_out", "dcb"]
+    for nm, a, r in zip(names, leaves, leaves64):
+        e = l2rel(a.grad.cpu().numpy(), r.grad.numpy())
+        assert e < TOL, f"{nm}: rel {e}"
+
+
+# ------------------------------------------------------------------ whole generator vs reference
+_train_models = {}
+
+
+def train_model(manifest, name):
+    m = manifest[name]
+    model = vrvq_amd.DAC_VRVQ(**m["kwargs"])
+    load_recipe(model, m["weight_seed"])
+    return model.to(DEV).train()
+
+
+def generator_step(model, g, m):
+    """The fixture's step (make_golden.train_fixture) on the HIP autograd path."""
+    x = t(g["audio_in"])
+    L = x.shape[-1]
+    torch.manual_seed(m["rng_seed"])
+    xp = model.preprocess(x, 44100)
+    z, feat = model.encoder(xp, return_feat=True)
+    z.retain_grad()
+    feat.retain_grad()
+    enc = model.quantizer(z, None, feat, 1)
+    zq = enc["z_q"]
+    zq.retain_grad()
+    y = model.decode(zq)[..., :L]
+    lam = m["lambdas"]
+    terms = {"waveform": (y - x).abs().mean(), "commitment": enc["commitment_loss"],
+             "codebook": enc["codebook_loss"], "rate": enc["imp_map"].mean()}
+    loss = sum(lam[k] * v for k, v in terms.items())
+    loss.backward()
+    return enc, y, z, feat, zq, terms, loss
+
+
+@pytest.mark.parametrize("name", ["golden_train_a2", "golden_train_a2_rows"])
+def test_generator_grads_vs_reference(manifest, name):
+    m = manifest[name]
+    g = load_golden(name)
+    model = train_model(manifest, name)
+    enc, y, z, feat, zq, terms, loss = generator_step(model, g, m)
+    # seed-controlled draws, bit-exact
+    kw = m["kwargs"]  # the fixture holds the raw torch.rand draws; scale them as the reference
+    lv = torch.from_numpy(g["draws_levels"]) * (kw["level_max"] - kw["level_min"]) + kw["level_min"]
+    np.testing.assert_array_equal(enc["random_levels"].numpy(), lv.numpy())
+    np.testing.assert_array_equal(enc["dropout"].numpy(), g["draws_dropout"])
+    np.testing.assert_array_equal(enc["codes"].cpu().numpy(), g["codes"])
+    np.testing.assert_allclose(enc["mask_imp"].detach().cpu().numpy(), g["mask_imp"], atol=1e-6)
+    assert rel_err(enc["imp_map"].detach().cpu().numpy(), g["imp_map"]) < TOL
+    assert rel_err(y.detach().cpu().numpy(), g["audio_out"]) < TOL
+    for k, v in terms.items():
+        assert float(v) == pytest.approx(float(g["term_" + k]), rel=TOL), k
+    for nm, a in (("grad_z_q", zq), ("grad_z", z), ("grad_feat", feat)):
+        e = l2rel(a.grad.cpu().numpy(), g[nm])
+        assert e < TOL, f"{nm}: rel {e}"
+    bad = []
+    params = dict(model.named_parameters())
+    assert sorted(params) == sorted(m["params"])
+    for pname in m["params"]:
+        gr = params[pname].grad.detach().reshape(-1).double().cpu()
+        ref_norm = m["grad_norms"][pname]
+        if abs(float(gr.norm()) - ref_norm) > TOL * max(ref_norm, 1e-30):
+            bad.append((pname, "norm", float(gr.norm()), ref_norm))
+        if "g_full/" + pname in g:
+            e = l2rel(gr.numpy(), g["g_full/" + pname])
+        else:
+            idx = np.unique(np.linspace(0, gr.numel() - 1, min(gr.numel(), 256)).round()
+                            .astype(np.int64))
+            e = l2rel(gr.numpy()[idx], g["g_s/" + pname])
+        if e > TOL:
+            bad.append((pname, "values", e))
+    assert not bad, bad[:10]
+
+
+def test_train_step_deterministic(manifest):
+    """Two identical seeded steps give bitwise identical gradients (fixed-order reductions)."""
+    name = "golden_train_a2"
+    m = manifest[name]
+    g = load_golden(name)
+    grads = []
+    for _ in range(2):
+        model = train_model(manifest, name)
+        generator_step(model, g, m)
+        grads.append([p.grad.detach().clone() for p in model.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)

@@ -85,11 +85,15 @@ def test_cpu_tensors_fail_loudly():
         model.encode(model.preprocess(x, 44100))
 
 
-def test_training_mode_not_silent():
-    model = vrvq_amd.DAC_VRVQ(n_codebooks=2)
+def test_training_mode_cpu_fails_loudly():
+    """Training mode runs the autograd kernels (vrvq_amd/train.py): on CPU tensors they raise
+    instead of falling back to a CPU implementation."""
+    model = vrvq_amd.DAC_VRVQ(n_codebooks=2, level_min=0.5, level_max=2.0)
     model.train()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="GPU"):
         model.quantizer(torch.zeros(1, 1024, 4), None, torch.zeros(1, 1024, 4), 1)
+    with pytest.raises(NotImplementedError):  # VBR quantizer in CBR mode: eval only
+        model.quantizer(torch.zeros(1, 1024, 4), 2, torch.zeros(1, 1024, 4), None)
 
 
 def test_invalid_model_type():

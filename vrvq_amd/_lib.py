@@ -48,6 +48,22 @@ SIGNATURES = {
     "vrvq_pack_codes": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "vrvq_unpack_offsets": [_P, _I, _I, _P, _P, _P],
     "vrvq_unpack_codes": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    # training step
+    "vrvq_wgrad_plan": [_I, _I, _I, _I, _I, _P, _P],
+    "vrvq_conv1d_wgrad": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P,
+                          ctypes.c_longlong, _P, _P],
+    "vrvq_snake_backward_workspace": [_I, _I, _I, _P],
+    "vrvq_snake_backward": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_longlong, _P],
+    "vrvq_bias_grad": [_P, _I, _I, _I, _P, _P],
+    "vrvq_act_backward": [_P, _P, ctypes.c_longlong, _I, _P, _P],
+    "vrvq_weight_norm_backward": [_P, _P, _P, _I, _I, _P, _P, _P],
+    "vrvq_pack_conv1d_flip": [_P, _I, _I, _I, _I, _P, _P],
+    "vrvq_mask_ste": [_P, _P, _P, _I, _I, _I, _F, _I, _I, _P, _P],
+    "vrvq_mask_ste_backward": [_P, _P, _P, _I, _I, _I, _F, _I, _P, _P],
+    "vrvq_rvq_expand_masked": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "vrvq_rvq_backward_workspace": [_I, _I, _I, _P],
+    "vrvq_rvq_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P,
+                          _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
 }
 EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)}
 

@@ -188,7 +188,8 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
   const int r0 = rb * 64 + rt * 16;
   if (r0 >= R) return;
   // D layout: lane l, reg q -> row 4*(l>>4) + q of the wave's 16, column (frame) l & 15
-  const int rr = r0 + 4 * lk;
+  const int rr = r0 + 4 * lk;  // R = 8 nq: rows rr..rr+3 are all valid iff rr < R
+  if (rr >= R) return;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int t = (cg * 3 + j) * 16 + lr;
@@ -558,6 +559,7 @@ struct ExpandArgs {
   const float* b_out;  // [nq][D]
   const float* imp;    // [B][T] or null
   float level;
+  const float* mask_in;  // [B][nq][T] or null: explicit mask values (training), replaces imp
   float* z_q_is;       // [B][nq][D][T] or null
   float* z_q;          // [B][D][T]
   float* mask;         // [B][nq][T] or null
@@ -613,7 +615,8 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
     for (int st = 0; st < 4; ++st) q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
     // k = 8: bias x 1 (lanes h = 0), k = 9: 0 x 0 (lanes h = 1)
     q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cb, h ? 0.0f : 1.0f, q, 0, 0, 0);
-    const float m = (s - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
+    const float m = a.mask_in ? (tv ? a.mask_in[((size_t)b * a.nq + i) * a.T + t] : 0.0f)
+                              : ((s - (float)i >= 0.0f) ? 1.0f : 0.0f);  // models/utils.py:45-61
     if (a.mask && ct == 0 && h == 0 && tv) a.mask[((size_t)b * a.nq + i) * a.T + t] = m;
     if (a.z_q_is && tv) {
       float* dst = a.z_q_is + (((size_t)b * a.nq + i) * a.D + c0 + 4 * h) * a.T + t;
@@ -686,8 +689,8 @@ int launch_chain(const ChainArgs& a0, int ncode, hipStream_t st) {
 
 int launch_expand(const float* zst, int batch, int dim, int frames, int nq, const float* w_out,
                   const float* b_out, const float* imp, float level, float* z_q_is, float* z_q,
-                  float* mask, hipStream_t st) {
-  ExpandArgs a{zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask};
+                  float* mask, hipStream_t st, const float* mask_in = nullptr) {
+  ExpandArgs a{zst, batch, dim, frames, nq, w_out, b_out, imp, level, mask_in, z_q_is, z_q, mask};
   a.n_ct = (dim + 31) / 32;
   a.n_tt = (frames + 31) / 32;
   const long long nblk = (long long)batch * a.n_tt * ((a.n_ct + 3) / 4);
@@ -768,6 +771,17 @@ extern "C" int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames,
   if (cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
   return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask,
                        as_stream(stream));
+}
+
+extern "C" int vrvq_rvq_expand_masked(const float* zst, int batch, int dim, int frames, int nq,
+                                      int cdim, const float* w_out, const float* b_out,
+                                      const float* mask, float* z_q_is, float* z_q,
+                                      vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(zst && w_out && b_out && mask && z_q);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim > 0);
+  if (cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
+  return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, nullptr, 1.0f, z_q_is, z_q,
+                       nullptr, as_stream(stream), mask);
 }
 
 extern "C" int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes) {

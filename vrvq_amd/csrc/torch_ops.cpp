@@ -537,6 +537,257 @@ std::tuple<Tensor, Tensor> unpack_codes(const Tensor& packed, const Tensor& coun
   return {codes, mask};
 }
 
+// --------------------------------------------------------------------------- training step
+// Backward operators of the generator (scripts/train.py:262-330), used by
+// the torch.autograd.Functions of vrvq_amd/train.py.
+
+// torch.nn.grad.conv1d_weight of a Snake-fused conv (include/vrvq.h, vrvq_conv1d_wgrad).
+Tensor conv1d_wgrad(const Tensor& a, const Tensor& x, int64_t k, int64_t stride, int64_t pad,
+                    int64_t dil, const optional<Tensor>& alpha_a,
+                    const optional<Tensor>& inv_alpha_a, const optional<Tensor>& alpha,
+                    const optional<Tensor>& inv_alpha) {
+  check_t(a, "a");
+  check_on(x, a, "x");
+  check_opt(alpha_a, a, "alpha_a");
+  check_opt(inv_alpha_a, a, "inv_alpha_a");
+  check_opt(alpha, a, "alpha");
+  check_opt(inv_alpha, a, "inv_alpha");
+  TORCH_CHECK(a.dim() == 3 && x.dim() == 3 && a.size(0) == x.size(0),
+              "conv1d_wgrad: a (B, M, Ta) and x (B, C, Tx) with the same batch");
+  TORCH_CHECK(alpha_a.has_value() == inv_alpha_a.has_value() &&
+                  alpha.has_value() == inv_alpha.has_value(),
+              "conv1d_wgrad: snake needs alpha and inv_alpha");
+  c10::DeviceGuard guard(a.device());
+  const int64_t B = a.size(0), M = a.size(1), TA = a.size(2), C = x.size(1), TX = x.size(2);
+  if (alpha_a.has_value()) TORCH_CHECK(alpha_a->numel() == M, "conv1d_wgrad: alpha_a per row of a");
+  if (alpha.has_value()) TORCH_CHECK(alpha->numel() == C, "conv1d_wgrad: alpha per channel of x");
+  int split = 0;
+  long long bytes = 0;
+  check_rc(vrvq_wgrad_plan((int)B, (int)M, (int)TA, (int)C, (int)k, &split, &bytes),
+           "vrvq_wgrad_plan");
+  Tensor ws = empty_f({(bytes + 3) / 4}, a);
+  Tensor out = empty_f({M, C, k}, a);
+  check_rc(vrvq_conv1d_wgrad(a.data_ptr<float>(), (int)B, (int)M, (int)TA, fp(alpha_a),
+                             fp(inv_alpha_a), x.data_ptr<float>(), (int)C, (int)TX, fp(alpha),
+                             fp(inv_alpha), (int)k, (int)stride, (int)pad, (int)dil, split,
+                             ws.data_ptr<float>(), (long long)ws.numel() * 4,
+                             out.data_ptr<float>(), stream_of(a)),
+           "vrvq_conv1d_wgrad");
+  return out;
+}
+
+// Snake1d backward (models/layers.py:26-32): (dx or empty, dalpha [C]).
+std::tuple<Tensor, Tensor> snake_backward(const Tensor& x, const Tensor& alpha,
+                                          const Tensor& inv_alpha, const Tensor& grad,
+                                          bool want_dx) {
+  check_t(x, "x");
+  check_on(alpha, x, "alpha");
+  check_on(inv_alpha, x, "inv_alpha");
+  check_on(grad, x, "grad");
+  TORCH_CHECK(x.dim() == 3 && grad.sizes() == x.sizes(), "snake_backward: x, grad (B, C, T)");
+  c10::DeviceGuard guard(x.device());
+  const int64_t B = x.size(0), C = x.size(1), T = x.size(2);
+  TORCH_CHECK(alpha.numel() == C && inv_alpha.numel() == C, "snake_backward: alpha per channel");
+  long long bytes = 0;
+  check_rc(vrvq_snake_backward_workspace((int)B, (int)C, (int)T, &bytes),
+           "vrvq_snake_backward_workspace");
+  Tensor ws = empty_f({(bytes + 3) / 4}, x);
+  Tensor dx = want_dx ? at::empty_like(x) : none_like(x);
+  Tensor da = empty_f({C}, x);
+  check_rc(vrvq_snake_backward(x.data_ptr<float>(), alpha.data_ptr<float>(),
+                               inv_alpha.data_ptr<float>(), grad.data_ptr<float>(), (int)B, (int)C,
+                               (int)T, opt_ptr(dx), da.data_ptr<float>(), ws.data_ptr<float>(),
+                               (long long)ws.numel() * 4, stream_of(x)),
+           "vrvq_snake_backward");
+  return {dx, da};
+}
+
+Tensor bias_grad(const Tensor& grad) {
+  check_t(grad, "grad");
+  TORCH_CHECK(grad.dim() == 3, "bias_grad: grad must be (B, C, T)");
+  c10::DeviceGuard guard(grad.device());
+  Tensor db = empty_f({grad.size(1)}, grad);
+  check_rc(vrvq_bias_grad(grad.data_ptr<float>(), (int)grad.size(0), (int)grad.size(1),
+                          (int)grad.size(2), db.data_ptr<float>(), stream_of(grad)),
+           "vrvq_bias_grad");
+  return db;
+}
+
+Tensor act_backward(const Tensor& y, const Tensor& grad, int64_t epilogue) {
+  check_t(y, "y");
+  check_on(grad, y, "grad");
+  TORCH_CHECK(grad.sizes() == y.sizes(), "act_backward: y and grad shapes differ");
+  c10::DeviceGuard guard(y.device());
+  Tensor out = at::empty_like(y);
+  check_rc(vrvq_act_backward(y.data_ptr<float>(), grad.data_ptr<float>(), (long long)y.numel(),
+                             (int)epilogue, out.data_ptr<float>(), stream_of(y)),
+           "vrvq_act_backward");
+  return out;
+}
+
+std::tuple<Tensor, Tensor> weight_norm_backward(const Tensor& g, const Tensor& v,
+                                                const Tensor& dw) {
+  check_t(g, "g");
+  check_on(v, g, "v");
+  check_on(dw, g, "dw");
+  TORCH_CHECK(dw.sizes() == v.sizes(), "weight_norm_backward: dw must have v's shape");
+  c10::DeviceGuard guard(v.device());
+  const int64_t rows = v.size(0), cols = v.numel() / rows;
+  TORCH_CHECK(g.numel() == rows, "weight_norm_backward: g must have one entry per row of v");
+  Tensor dg = at::empty_like(g), dv = at::empty_like(v);
+  check_rc(vrvq_weight_norm_backward(g.data_ptr<float>(), v.data_ptr<float>(),
+                                     dw.data_ptr<float>(), (int)rows, (int)cols,
+                                     dg.data_ptr<float>(), dv.data_ptr<float>(), stream_of(v)),
+           "vrvq_weight_norm_backward");
+  return {dg, dv};
+}
+
+// Packed adjoint of a stride-1 Conv1d weight (input gradient = conv1d of dY with it).
+Tensor pack_conv1d_flip(const Tensor& w) {
+  check_t(w, "w");
+  TORCH_CHECK(w.dim() == 3, "pack_conv1d_flip: w must be (Cout, Cin, k)");
+  c10::DeviceGuard guard(w.device());
+  const int64_t cout = w.size(0), cin = w.size(1), k = w.size(2);
+  const int64_t cin_pad = round_up(cin, 128);
+  Tensor wp = empty_f({cout, k, cin_pad}, w);
+  check_rc(vrvq_pack_conv1d_flip(w.data_ptr<float>(), (int)cout, (int)cin, (int)k, (int)cin_pad,
+                                 wp.data_ptr<float>(), stream_of(w)),
+           "vrvq_pack_conv1d_flip");
+  return wp;
+}
+
+// Training mask (models/quantize.py:377-414).
+Tensor mask_ste(const Tensor& imp, const Tensor& levels, const optional<Tensor>& dropout,
+                int64_t nq, double alpha, int64_t n_imps, int64_t n_drop) {
+  check_t(imp, "imp");
+  check_on(levels, imp, "levels");
+  if (dropout.has_value()) check_on(*dropout, imp, "dropout", at::kLong);
+  const int64_t B = imp.size(0), T = imp.size(-1);
+  TORCH_CHECK(imp.numel() == B * T && levels.numel() == B, "mask_ste: imp (B, 1, T), levels (B)");
+  if (dropout.has_value()) TORCH_CHECK(dropout->numel() == B, "mask_ste: dropout (B)");
+  c10::DeviceGuard guard(imp.device());
+  Tensor mask = empty_f({B, nq, T}, imp);
+  check_rc(vrvq_mask_ste(imp.data_ptr<float>(), levels.data_ptr<float>(),
+                         dropout.has_value() ? dropout->data_ptr<int64_t>() : nullptr, (int)B,
+                         (int)T, (int)nq, (float)alpha, (int)n_imps, (int)n_drop,
+                         mask.data_ptr<float>(), stream_of(imp)),
+           "vrvq_mask_ste");
+  return mask;
+}
+
+Tensor mask_ste_backward(const Tensor& imp, const Tensor& levels, const Tensor& dmask,
+                         double alpha, int64_t n_imps) {
+  check_t(imp, "imp");
+  check_on(levels, imp, "levels");
+  check_on(dmask, imp, "dmask");
+  const int64_t B = imp.size(0), T = imp.size(-1);
+  TORCH_CHECK(dmask.dim() == 3 && dmask.size(0) == B && dmask.size(2) == T,
+              "mask_ste_backward: dmask (B, nq, T)");
+  c10::DeviceGuard guard(imp.device());
+  Tensor dimp = at::empty_like(imp);
+  check_rc(vrvq_mask_ste_backward(imp.data_ptr<float>(), levels.data_ptr<float>(),
+                                  dmask.data_ptr<float>(), (int)B, (int)T, (int)dmask.size(1),
+                                  (float)alpha, (int)n_imps, dimp.data_ptr<float>(),
+                                  stream_of(imp)),
+           "vrvq_mask_ste_backward");
+  return dimp;
+}
+
+// Training-mode quantizer forward: all stages (projection + chain) and the masked expansion
+// with explicit mask values; returns the state the backward needs (zst).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode_train(
+    const Tensor& z, const Tensor& w_in_t, const Tensor& b_in, const Tensor& cb,
+    const Tensor& cbf, const Tensor& c2, const Tensor& w_out, const Tensor& b_out,
+    const Tensor& mcol, const Tensor& qb, const Tensor& mask) {
+  check_t(z, "z");
+  TORCH_CHECK(z.dim() == 3, "rvq_encode_train: z must be (B, D, T)");
+  check_rvq_weights(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out);
+  check_on(mcol, z, "mcol");
+  check_on(qb, z, "qb");
+  check_on(mask, z, "mask");
+  c10::DeviceGuard guard(z.device());
+  const int64_t B = z.size(0), D = z.size(1), T = z.size(2);
+  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2);
+  TORCH_CHECK(mask.sizes() == at::IntArrayRef({B, nq, T}), "rvq_encode_train: mask (B, nq, T)");
+  TORCH_CHECK(mcol.numel() == nq * nq * d * d && qb.numel() == nq * d,
+              "rvq_encode_train: cross terms (rvq_cross_prep) do not match nq");
+  Tensor codes = at::empty({B, nq, T}, z.options().dtype(at::kLong));
+  Tensor latents = empty_f({B, nq * d, T}, z);
+  Tensor loss_pf = empty_f({B, nq, T}, z);
+  Tensor zst = empty_f({B, nq, T, d}, z);
+  Tensor z_q = empty_f({B, D, T}, z);
+  Tensor part = empty_f({8 * B * T * nq * d}, z);
+  void* st = stream_of(z);
+  check_rc(vrvq_rvq_project(z.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)d,
+                            w_in_t.data_ptr<float>(), part.data_ptr<float>(), st),
+           "vrvq_rvq_project");
+  check_rc(vrvq_rvq_chain(part.data_ptr<float>(), (int)B, (int)T, (int)nq, (int)N, (int)d,
+                          b_in.data_ptr<float>(), qb.data_ptr<float>(), mcol.data_ptr<float>(),
+                          cb.data_ptr<float>(), cbf.data_ptr<float>(), c2.data_ptr<float>(),
+                          nullptr, 1.0f, codes.data_ptr<int64_t>(), latents.data_ptr<float>(),
+                          loss_pf.data_ptr<float>(), zst.data_ptr<float>(), nullptr, st),
+           "vrvq_rvq_chain");
+  check_rc(vrvq_rvq_expand_masked(zst.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)d,
+                                  w_out.data_ptr<float>(), b_out.data_ptr<float>(),
+                                  mask.data_ptr<float>(), nullptr, z_q.data_ptr<float>(), st),
+           "vrvq_rvq_expand_masked");
+  return {codes, latents, loss_pf, zst, z_q};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_backward(
+    const Tensor& dz_q, const Tensor& g_commit, const Tensor& g_codebook, const Tensor& z,
+    const Tensor& zst, const Tensor& latents, const Tensor& codes, const Tensor& mask,
+    const Tensor& w_in_t, const Tensor& w_out, const Tensor& b_out, const Tensor& mcol,
+    const Tensor& cb) {
+  check_t(dz_q, "dz_q");
+  check_on(g_commit, dz_q, "g_commit");
+  check_on(g_codebook, dz_q, "g_codebook");
+  check_on(z, dz_q, "z");
+  check_on(zst, dz_q, "zst");
+  check_on(latents, dz_q, "latents");
+  check_on(codes, dz_q, "codes", at::kLong);
+  check_on(mask, dz_q, "mask");
+  check_on(w_in_t, dz_q, "w_in_t");
+  check_on(w_out, dz_q, "w_out");
+  check_on(b_out, dz_q, "b_out");
+  check_on(mcol, dz_q, "mcol");
+  check_on(cb, dz_q, "cb");
+  TORCH_CHECK(g_commit.numel() == 1 && g_codebook.numel() == 1,
+              "rvq_backward: loss gradients are scalars");
+  c10::DeviceGuard guard(dz_q.device());
+  const int64_t B = z.size(0), D = z.size(1), T = z.size(2);
+  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2);
+  TORCH_CHECK(dz_q.sizes() == z.sizes(), "rvq_backward: dz_q must have z's shape");
+  TORCH_CHECK(zst.sizes() == at::IntArrayRef({B, nq, T, d}) &&
+                  latents.sizes() == at::IntArrayRef({B, nq * d, T}) &&
+                  codes.sizes() == at::IntArrayRef({B, nq, T}) && mask.sizes() == codes.sizes(),
+              "rvq_backward: forward state shapes");
+  TORCH_CHECK(w_in_t.sizes() == at::IntArrayRef({nq, D, d}) && w_out.sizes() == w_in_t.sizes() &&
+                  b_out.numel() == nq * D && mcol.numel() == nq * nq * d * d,
+              "rvq_backward: weight shapes");
+  long long bytes = 0;
+  check_rc(vrvq_rvq_backward_workspace((int)B, (int)T, (int)nq, &bytes),
+           "vrvq_rvq_backward_workspace");
+  Tensor ws = empty_f({(bytes + 3) / 4}, z);
+  Tensor dz = at::empty_like(z), dmask = at::empty_like(mask);
+  Tensor dw_in = empty_f({nq, d, D}, z), db_in = empty_f({nq, d}, z);
+  Tensor dw_out = empty_f({nq, D, d}, z), db_out = empty_f({nq, D}, z);
+  Tensor dcb = at::empty_like(cb);
+  check_rc(vrvq_rvq_backward(dz_q.data_ptr<float>(), g_commit.data_ptr<float>(),
+                             g_codebook.data_ptr<float>(), z.data_ptr<float>(),
+                             zst.data_ptr<float>(), latents.data_ptr<float>(),
+                             codes.data_ptr<int64_t>(), mask.data_ptr<float>(), (int)B, (int)D,
+                             (int)T, (int)nq, (int)N, (int)d, w_in_t.data_ptr<float>(),
+                             w_out.data_ptr<float>(), b_out.data_ptr<float>(),
+                             mcol.data_ptr<float>(), cb.data_ptr<float>(), dz.data_ptr<float>(),
+                             dmask.data_ptr<float>(), dw_in.data_ptr<float>(),
+                             db_in.data_ptr<float>(), dw_out.data_ptr<float>(),
+                             db_out.data_ptr<float>(), dcb.data_ptr<float>(), ws.data_ptr<float>(),
+                             (long long)ws.numel() * 4, stream_of(z)),
+           "vrvq_rvq_backward");
+  return {dz, dmask, dw_in, db_in, dw_out, db_out, dcb};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(vrvq, m) {
@@ -580,6 +831,30 @@ TORCH_LIBRARY(vrvq, m) {
   m.def(
       "unpack_codes(Tensor packed, Tensor counts, Tensor clip_off, int n_codebooks) "
       "-> (Tensor, Tensor)");
+  m.def(
+      "conv1d_wgrad(Tensor a, Tensor x, int k, int stride, int pad, int dil, Tensor? alpha_a, "
+      "Tensor? inv_alpha_a, Tensor? alpha, Tensor? inv_alpha) -> Tensor");
+  m.def(
+      "snake_backward(Tensor x, Tensor alpha, Tensor inv_alpha, Tensor grad, bool want_dx) "
+      "-> (Tensor, Tensor)");
+  m.def("bias_grad(Tensor grad) -> Tensor");
+  m.def("act_backward(Tensor y, Tensor grad, int epilogue) -> Tensor");
+  m.def("weight_norm_backward(Tensor g, Tensor v, Tensor dw) -> (Tensor, Tensor)");
+  m.def("pack_conv1d_flip(Tensor w) -> Tensor");
+  m.def(
+      "mask_ste(Tensor imp, Tensor levels, Tensor? dropout, int nq, float alpha, int n_imps, "
+      "int n_drop) -> Tensor");
+  m.def(
+      "mask_ste_backward(Tensor imp, Tensor levels, Tensor dmask, float alpha, int n_imps) "
+      "-> Tensor");
+  m.def(
+      "rvq_encode_train(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
+      "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor mask) "
+      "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "rvq_backward(Tensor dz_q, Tensor g_commit, Tensor g_codebook, Tensor z, Tensor zst, "
+      "Tensor latents, Tensor codes, Tensor mask, Tensor w_in_t, Tensor w_out, Tensor b_out, "
+      "Tensor mcol, Tensor cb) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
 }
 
 #define VRVQ_IMPLS(m) \
@@ -605,6 +880,16 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("pack_codes", &pack_codes); \
   m.impl("unpack_offsets", &unpack_offsets); \
   m.impl("unpack_codes", &unpack_codes); \
+  m.impl("conv1d_wgrad", &conv1d_wgrad); \
+  m.impl("snake_backward", &snake_backward); \
+  m.impl("bias_grad", &bias_grad); \
+  m.impl("act_backward", &act_backward); \
+  m.impl("weight_norm_backward", &weight_norm_backward); \
+  m.impl("pack_conv1d_flip", &pack_conv1d_flip); \
+  m.impl("mask_ste", &mask_ste); \
+  m.impl("mask_ste_backward", &mask_ste_backward); \
+  m.impl("rvq_encode_train", &rvq_encode_train); \
+  m.impl("rvq_backward", &rvq_backward); \
 
 TORCH_LIBRARY_IMPL(vrvq, CUDA, m) { VRVQ_IMPLS(m) }
 

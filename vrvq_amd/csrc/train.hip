@@ -1,0 +1,327 @@
+// Backward kernels of the VRVQ generator (the training step, SURVEY.md §8f row 1;
+// scripts/train.py:262-335): weight gradients of the Snake-fused convolutions, Snake /
+// activation / bias / weight-norm backward, and the adjoint-conv weight packing that lets the
+// input gradient reuse the forward MFMA conv kernels (conv.hip):
+//   Conv1d (stride 1, dilation d):   dXs = conv1d(dY, W^flip, pad' = d (K-1) - pad)
+//   Conv1d (k = 2s, stride s):       dXs = conv_transpose1d(dY, W) (the polyphase kernel)
+//   ConvTranspose1d (k = 2s):        dXs = conv1d(dY, W, stride s, pad)
+// Every reduction is deterministic (fixed order; split-K partials summed in split order).
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient as a split-K GEMM on v_mfma_f32_32x32x2_f32:
+//   out[m][c][k] = sum_b sum_{t < TA} A[b][m][t] * Xs[b][c][t*s - p + k*d]
+//   Xs = snake(X) when alpha != NULL (the layer's input activation), 0 outside [0, TX)
+//   As = snake(A) when alpha_a != NULL
+// Conv1d:          A = dY (m = Cout), X = the layer input (c = Cin)   -> dW[Cout][Cin][K]
+// ConvTranspose1d: A = the layer input (m = Cin, snake on A), X = dY  -> dW[Cin][Cout][K]
+//                  (y[co][t s - p + k] += W[ci][co][k] xs[ci][t])
+// Workgroup = (64 m x 64 c tile, tap k, split); 4 waves of 32 x 32; K_red chunks of 32
+// (b, t) values staged in LDS; partial[split][m][c][k] reduced in split order afterwards.
+constexpr int WG_BM = 64, WG_BN = 64, WG_KT = 32;
+
+struct WgradArgs {
+  const float* A; int M, TA;
+  const float* X; int C, TX;
+  const float* alpha_a; const float* inv_alpha_a;
+  const float* alpha; const float* inv_alpha;
+  int B, K, s, p, d;
+  int n_split, chunks;   // total (b, t-chunk) chunks, split evenly over n_split
+  float* part;           // [n_split][M][C][K]
+};
+
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  __shared__ float A_s[WG_BM][WG_KT + 1];
+  __shared__ float X_s[WG_BN][WG_KT + 1];
+  const int n_mt = (a.M + WG_BM - 1) / WG_BM, n_ct = (a.C + WG_BN - 1) / WG_BN;
+  int bid = blockIdx.x;
+  const int mt = bid % n_mt; bid /= n_mt;
+  const int ct = bid % n_ct; bid /= n_ct;
+  const int k = bid % a.K;
+  const int sp = bid / a.K;
+  const int m0 = mt * WG_BM, c0 = ct * WG_BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int nct = (a.TA + WG_KT - 1) / WG_KT;
+  const int q0 = (int)((long long)sp * a.chunks / a.n_split);
+  const int q1 = (int)((long long)(sp + 1) * a.chunks / a.n_split);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int q = q0; q < q1; ++q) {
+    const int b = q / nct, t0 = (q - b * nct) * WG_KT;
+    // stage A[b][m0..+64][t0..+32] and Xs[b][c0..+64][(t0..+32)*s - p + k*d]
+    for (int e = tid; e < WG_BM * WG_KT; e += 256) {
+      const int r = e / WG_KT, j = e - r * WG_KT;
+      const int m = m0 + r, t = t0 + j;
+      float av = 0.0f;
+      if (m < a.M && t < a.TA) {
+        av = a.A[((size_t)b * a.M + m) * a.TA + t];
+        if (a.alpha_a) av = snake_act(av, a.alpha_a[m], a.inv_alpha_a[m]);
+      }
+      A_s[r][j] = av;
+      const int c = c0 + r;
+      const int tx = t * a.s - a.p + k * a.d;
+      float v = 0.0f;
+      if (c < a.C && t < a.TA && tx >= 0 && tx < a.TX) {
+        v = a.X[((size_t)b * a.C + c) * a.TX + tx];
+        if (a.alpha) v = snake_act(v, a.alpha[c], a.inv_alpha[c]);
+      }
+      X_s[r][j] = v;
+    }
+    __syncthreads();
+    // 32x32x2: A lane l -> A[m = l & 31][kr = l >> 5]; B lane l -> B[kr = l >> 5][n = l & 31]
+#pragma unroll
+    for (int kk = 0; kk < WG_KT; kk += 2) {
+      const float av = A_s[wm * 32 + (lane & 31)][kk + (lane >> 5)];
+      const float bv = X_s[wn * 32 + (lane & 31)][kk + (lane >> 5)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D: lane l, reg r -> row (r & 3) + 8 (r >> 2) + 4 (l >> 5), col l & 31
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int c = c0 + wn * 32 + (lane & 31);
+    if (m < a.M && c < a.C)
+      a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k] = acc[r];
+  }
+}
+
+// out[e] = sum_{s < n} part[s][e], split order
+__global__ void split_reduce_kernel(const float* __restrict__ part, size_t n_elem, int n_split,
+                                    float* __restrict__ out) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n_elem;
+       e += (size_t)gridDim.x * blockDim.x) {
+    float acc = part[e];
+    for (int s = 1; s < n_split; ++s) acc = acc + part[(size_t)s * n_elem + e];
+    out[e] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Snake backward (models/layers.py:26-32 under torch autograd):
+//   y = x + inv * sin(a x)^2,  inv = 1 / (a + 1e-9)
+//   dx = g * (1 + inv * (2 sin(a x) cos(a x)) * a)
+//   da = sum_{b,t} g * (-inv^2 * sin(a x)^2 + inv * (2 sin(a x) cos(a x)) * x)
+// One workgroup per (channel, split of the batch*time range); dalpha partials [split][C].
+__global__ __launch_bounds__(256) void snake_backward_kernel(
+    const float* __restrict__ x, const float* __restrict__ alpha,
+    const float* __restrict__ inv_alpha, const float* __restrict__ g, int B, int C, int T,
+    int n_split, float* __restrict__ dx, float* __restrict__ da_part) {
+  __shared__ float red[256];
+  const int c = blockIdx.x % C, sp = blockIdx.x / C;
+  const float a = alpha[c], inv = inv_alpha[c];
+  const long long n = (long long)B * T;
+  const long long e0 = n * sp / n_split, e1 = n * (sp + 1) / n_split;
+  float acc = 0.0f;
+  for (long long e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int b = (int)(e / T), t = (int)(e - (long long)b * T);
+    const size_t o = ((size_t)b * C + c) * T + t;
+    const float xv = x[o], gv = g[o];
+    const float sn = sinf(a * xv), cs = cosf(a * xv);
+    const float s2 = (2.0f * sn) * cs;
+    if (dx) dx[o] = gv * (1.0f + (inv * s2) * a);
+    acc += gv * (-(inv * inv) * (sn * sn) + (inv * s2) * xv);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && da_part) da_part[(size_t)sp * C + c] = red[0];
+}
+
+// db[c] (+)= sum_{b,t} g[b][c][t]; one workgroup per channel (fixed order)
+__global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ g, int B, int C,
+                                                        int T, float* __restrict__ db) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float acc = 0.0f;
+  for (long long e = threadIdx.x; e < (long long)B * T; e += 256) {
+    const int b = (int)(e / T), t = (int)(e - (long long)b * T);
+    acc += g[((size_t)b * C + c) * T + t];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) db[c] = red[0];
+}
+
+// tanh / sigmoid backward from the stored output y (models/dac_vrvq.py:74,
+// models/importance_subnet.py:44)
+__global__ void act_backward_kernel(const float* __restrict__ y, const float* __restrict__ g,
+                                    size_t n, int epi, float* __restrict__ out) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const float yv = y[e], gv = g[e];
+    out[e] = epi == VRVQ_EPI_TANH ? gv * (1.0f - yv * yv) : gv * (yv * (1.0f - yv));
+  }
+}
+
+// torch.nn.utils.weight_norm backward, per row r (norm over the other dims):
+//   n = ||v_r||, dg_r = (dw_r . v_r) / n, dv_r = (g_r / n) (dw_r - v_r (dw_r . v_r) / n^2)
+__global__ __launch_bounds__(256) void weight_norm_backward_kernel(
+    const float* __restrict__ g, const float* __restrict__ v, const float* __restrict__ dw,
+    int cols, float* __restrict__ dg, float* __restrict__ dv) {
+  __shared__ float r1[256], r2[256];
+  const size_t row = blockIdx.x;
+  const float* vr = v + row * cols;
+  const float* dr = dw + row * cols;
+  float ss = 0.0f, dot = 0.0f;
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    ss = fmaf(vr[c], vr[c], ss);
+    dot = fmaf(dr[c], vr[c], dot);
+  }
+  r1[threadIdx.x] = ss;
+  r2[threadIdx.x] = dot;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      r1[threadIdx.x] += r1[threadIdx.x + h];
+      r2[threadIdx.x] += r2[threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  const float n = sqrtf(r1[0]), dvv = r2[0];
+  const float gr = g[row];
+  if (threadIdx.x == 0) dg[row] = dvv / n;
+  const float sc = gr / n, corr = dvv / (n * n);
+  for (int c = threadIdx.x; c < cols; c += 256) dv[row * cols + c] = sc * (dr[c] - vr[c] * corr);
+}
+
+// Adjoint-conv packing: the input gradient of a stride-1 Conv1d is a Conv1d of dY with
+//   W'[ci][co][k] = W[co][ci][K-1-k], packed as vrvq_pack_conv1d_weight would pack W':
+//   wp[co][k][ci_pad] (Cin' = Cout rows of K taps, Cout' = Cin padded to cout_pad)
+__global__ void pack_conv1d_flip_kernel(const float* __restrict__ w, int cout, int cin, int K,
+                                        int cin_pad, float* __restrict__ wp) {
+  const size_t total = (size_t)cout * K * cin_pad;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin_pad);
+    const size_t rk = i / cin_pad;
+    const int k = (int)(rk % K);
+    const int co = (int)(rk / K);
+    wp[i] = ci < cin ? w[((size_t)co * cin + ci) * K + (K - 1 - k)] : 0.0f;
+  }
+}
+
+unsigned grid_n(size_t total, unsigned block) {
+  size_t g = (total + block - 1) / block;
+  return (unsigned)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+}  // namespace
+
+extern "C" int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_split,
+                               long long* workspace_bytes) {
+  VRVQ_CHECK_ARG(n_split && workspace_bytes && batch > 0 && m > 0 && ta > 0 && c > 0 && k > 0);
+  const long long tiles = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) * k;
+  const long long chunks = (long long)batch * ((ta + WG_KT - 1) / WG_KT);
+  long long s = (1024 + tiles - 1) / tiles;  // >= 4 workgroups per CU in total
+  if (s > chunks) s = chunks;
+  if (s > 256) s = 256;
+  if (s < 1) s = 1;
+  *n_split = (int)s;
+  *workspace_bytes = s * m * (long long)c * k * (long long)sizeof(float);
+  return 0;
+}
+
+extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
+                                 const float* alpha_a, const float* inv_alpha_a, const float* x,
+                                 int c, int tx, const float* alpha, const float* inv_alpha, int k,
+                                 int stride, int pad, int dil, int n_split, float* workspace,
+                                 long long workspace_bytes, float* out, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(a && x && out && workspace && batch > 0 && m > 0 && ta > 0 && c > 0 && tx > 0);
+  VRVQ_CHECK_ARG(k > 0 && stride > 0 && pad >= 0 && dil > 0 && n_split > 0);
+  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
+  VRVQ_CHECK_ARG(alpha_a == nullptr || inv_alpha_a != nullptr);
+  VRVQ_CHECK_ARG(workspace_bytes >= (long long)n_split * m * (long long)c * k * 4);
+  WgradArgs w{a, m, ta, x, c, tx, alpha_a, inv_alpha_a, alpha, inv_alpha, batch, k, stride, pad,
+              dil, n_split, 0, workspace};
+  w.chunks = batch * ((ta + WG_KT - 1) / WG_KT);
+  if (w.n_split > w.chunks) w.n_split = w.chunks;
+  const long long nblk = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) * k *
+                         w.n_split;
+  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, st, w);
+  const size_t n_elem = (size_t)m * c * k;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid_n(n_elem, 256)), dim3(256), 0, st, workspace,
+                     n_elem, w.n_split, out);
+  return vrvq_launch_status();
+}
+
+static int snake_split(int batch, int frames) {
+  const long long n = (long long)batch * frames;
+  long long s = (n + 65535) / 65536;
+  return (int)(s > 64 ? 64 : (s < 1 ? 1 : s));
+}
+
+extern "C" int vrvq_snake_backward_workspace(int batch, int channels, int frames,
+                                             long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && channels > 0 && frames > 0);
+  *bytes = (long long)snake_split(batch, frames) * channels * (long long)sizeof(float);
+  return 0;
+}
+
+extern "C" int vrvq_snake_backward(const float* x, const float* alpha, const float* inv_alpha,
+                                   const float* grad, int batch, int channels, int frames,
+                                   float* dx, float* dalpha, float* workspace,
+                                   long long workspace_bytes, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && alpha && inv_alpha && grad && (dx || dalpha) && batch > 0 &&
+                 channels > 0 && frames > 0);
+  const int n_split = snake_split(batch, frames);
+  if (dalpha) VRVQ_CHECK_ARG(workspace && workspace_bytes >= (long long)n_split * channels * 4);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(snake_backward_kernel, dim3((unsigned)(channels * n_split)), dim3(256), 0, st,
+                     x, alpha, inv_alpha, grad, batch, channels, frames, n_split, dx,
+                     dalpha ? workspace : nullptr);
+  if (dalpha)
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(grid_n(channels, 256)), dim3(256), 0, st,
+                       workspace, (size_t)channels, n_split, dalpha);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_bias_grad(const float* grad, int batch, int channels, int frames, float* db,
+                              vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(grad && db && batch > 0 && channels > 0 && frames > 0);
+  hipLaunchKernelGGL(bias_grad_kernel, dim3(channels), dim3(256), 0, as_stream(stream), grad, batch,
+                     channels, frames, db);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_act_backward(const float* y, const float* grad, long long n, int epilogue,
+                                 float* out, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(y && grad && out && n > 0);
+  VRVQ_CHECK_ARG(epilogue == VRVQ_EPI_TANH || epilogue == VRVQ_EPI_SIGMOID);
+  hipLaunchKernelGGL(act_backward_kernel, dim3(grid_n((size_t)n, 256)), dim3(256), 0,
+                     as_stream(stream), y, grad, (size_t)n, epilogue, out);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_weight_norm_backward(const float* g, const float* v, const float* dw, int rows,
+                                         int cols, float* dg, float* dv, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(g && v && dw && dg && dv && rows > 0 && cols > 0);
+  hipLaunchKernelGGL(weight_norm_backward_kernel, dim3(rows), dim3(256), 0, as_stream(stream), g,
+                     v, dw, cols, dg, dv);
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_pack_conv1d_flip(const float* w, int cout, int cin, int k, int cin_pad,
+                                     float* w_packed, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w && w_packed && cout > 0 && cin > 0 && k > 0 && cin_pad >= cin);
+  const size_t total = (size_t)cout * k * cin_pad;
+  hipLaunchKernelGGL(pack_conv1d_flip_kernel, dim3(grid_n(total, 256)), dim3(256), 0,
+                     as_stream(stream), w, cout, cin, k, cin_pad, w_packed);
+  return vrvq_launch_status();
+}

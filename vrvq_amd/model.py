@@ -14,7 +14,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, train
 from .layers import (DecoderBlock, EncoderBlock, ResidualUnit, Snake1d, WNConv1d,
                      WNConvTranspose1d, _param_key)
 
@@ -33,6 +33,9 @@ class Encoder(nn.Module):
         self.block = nn.Sequential(*blocks)
 
     def forward(self, x, return_feat: bool = False):
+        if self.training:  # autograd path (vrvq_amd/train.py)
+            out, feat = train.encoder_forward(self, x)
+            return (out, feat) if return_feat else out
         # Chained launches: every conv's epilogue also writes the next Snake's output, so each
         # activation is evaluated once per element (include/vrvq.h, producer-side Snake).
         n = len(self.block)
@@ -63,6 +66,8 @@ class Decoder(nn.Module):
         self.model = nn.Sequential(*layers)
 
     def forward(self, x):
+        if self.training:
+            return train.decoder_forward(self, x)
         n = len(self.model)
         _, x_snk = self.model[0](x, out_snake=self.model[1].entry_snake(), want_raw=False)
         for i in range(1, n - 3):
@@ -87,9 +92,11 @@ class ImportanceSubnet(nn.Module):
             for i in range(len(in_ch))
         ])
         self.act_fn = nn.Sigmoid()
-        self.detach_input = detach_input  # forward-only here: detach is a no-op
+        self.detach_input = detach_input  # detaches the input in training (no grad to feat)
 
     def forward(self, x_in):
+        if self.training:
+            return train.imp_subnet_forward(self, x_in)
         x = self.in_block[1](x_in, snake=self.in_block[0])
         last = len(self.blocks) - 1
         for i, blk in enumerate(self.blocks):
@@ -189,15 +196,9 @@ class ResidualVectorQuantize(nn.Module):
             self._stack_cache = (key, _Stacked(self.quantizers, params[0].device))
         return self._stack_cache[1]
 
-    def _check_mode(self):
-        if self.training:
-            raise NotImplementedError(
-                "vrvq_amd implements the inference path; the training-mode quantizer "
-                "(quantizer dropout / random levels, models/quantize.py:175-194, 374-414) is "
-                "the next row of SURVEY.md §8f — call .eval()")
-
     def forward(self, z, n_quantizers: int = None):
-        self._check_mode()
+        if self.training:  # quantizer dropout, autograd (models/quantize.py:175-199)
+            return train.cbr_forward(self, z.contiguous())
         n = self.n_codebooks if n_quantizers is None else min(int(n_quantizers), self.n_codebooks)
         st = self.stacked()
         if n < self.n_codebooks:
@@ -259,7 +260,13 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
 
     def forward(self, z: torch.Tensor, n_quantizers: int = None, feat_enc: torch.Tensor = None,
                 level: float = None, want_z_q_is: bool = True):
-        self._check_mode()
+        if n_quantizers is None and level is None:
+            raise AssertionError("level must be specified in VBR mode")
+        if self.training:
+            if n_quantizers is not None:
+                raise NotImplementedError("VBR quantizer in CBR mode is eval-only")
+            # random levels / dropout / full-codebook rows, autograd (models/quantize.py:374-414)
+            return train.vbr_forward(self, z.contiguous(), feat_enc.contiguous())
         B, D, T = z.shape
         nq = self.n_codebooks
         if n_quantizers is None:

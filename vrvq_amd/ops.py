@@ -206,6 +206,66 @@ def bpf(mask: torch.Tensor, bits: torch.Tensor) -> torch.Tensor:
     return _ops().bpf(mask, bits)
 
 
+# ----------------------------------------------------------------------------- training step
+# Backward operators of the generator (include/vrvq.h "Training step"; vrvq_amd/train.py).
+def conv1d_wgrad(a, x, k: int, stride: int = 1, pad: int = 0, dil: int = 1,
+                 snake_a: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 snake_x: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """out[m][c][k] = sum_{b,t} snake_a(a)[b][m][t] * snake_x(x)[b][c][t*stride - pad + k*dil]
+    (split-K MFMA GEMM, fixed reduction order)."""
+    aa, ia = snake_a if snake_a is not None else (None, None)
+    ax, ix = snake_x if snake_x is not None else (None, None)
+    return _ops().conv1d_wgrad(a, x, int(k), int(stride), int(pad), int(dil), aa, ia, ax, ix)
+
+
+def snake_backward(x, alpha, inv_alpha, grad, want_dx: bool = True):
+    """Snake1d backward: (dx or None, dalpha [C])."""
+    dx, da = _ops().snake_backward(x, alpha, inv_alpha, grad, bool(want_dx))
+    return _none(dx), da
+
+
+def bias_grad(grad: torch.Tensor) -> torch.Tensor:
+    return _ops().bias_grad(grad)
+
+
+def act_backward(y: torch.Tensor, grad: torch.Tensor, epilogue: int) -> torch.Tensor:
+    return _ops().act_backward(y, grad, int(epilogue))
+
+
+def weight_norm_backward(g, v, dw):
+    """(dg, dv) of w = v * (g / ||v||) (norm over all dims but 0)."""
+    return _ops().weight_norm_backward(g, v, dw)
+
+
+def pack_conv1d_flip(w: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """Packed adjoint (flipped, transposed) weight of a stride-1 Conv1d."""
+    wp = _ops().pack_conv1d_flip(w)
+    return wp, wp.shape[2]
+
+
+def mask_ste(imp, levels, dropout, nq: int, alpha: float, n_imps: int, n_drop: int):
+    """Training-mode mask (models/quantize.py:377-414): importance STE rows, dropout rows,
+    full-codebook rows."""
+    return _ops().mask_ste(imp, levels, dropout, int(nq), float(alpha), int(n_imps), int(n_drop))
+
+
+def mask_ste_backward(imp, levels, dmask, alpha: float, n_imps: int):
+    return _ops().mask_ste_backward(imp, levels, dmask, float(alpha), int(n_imps))
+
+
+def rvq_encode_train(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, mask):
+    """Training-mode quantizer forward: (codes, latents, loss_pf, zst, z_q) with z_q masked by
+    the given mask values."""
+    return _ops().rvq_encode_train(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, mask)
+
+
+def rvq_backward(dz_q, g_commit, g_codebook, z, zst, latents, codes, mask, w_in_t, w_out, b_out,
+                 mcol, cb):
+    """(dz, dmask, dw_in [nq,d,D], db_in, dw_out [nq,D,d], db_out, dcb)."""
+    return _ops().rvq_backward(dz_q, g_commit, g_codebook, z, zst, latents, codes, mask, w_in_t,
+                               w_out, b_out, mcol, cb)
+
+
 # ----------------------------------------------------------------------------- fake kernels
 def _register_fakes():
     """Shape functions of every op (FakeTensorMode / meta / torch.compile tracing)."""
@@ -334,3 +394,50 @@ def _register_fakes():
         B, T = counts.shape
         return (counts.new_empty((B, n_codebooks, T), dtype=torch.int64),
                 counts.new_empty((B, n_codebooks, T), dtype=torch.float32))
+
+    @reg("vrvq::conv1d_wgrad")
+    def _(a, x, k, stride, pad, dil, alpha_a, inv_alpha_a, alpha, inv_alpha):
+        return f32(a, (a.shape[1], x.shape[1], k))
+
+    @reg("vrvq::snake_backward")
+    def _(x, alpha, inv_alpha, grad, want_dx):
+        return (torch.empty_like(x) if want_dx else none(x)), f32(x, (x.shape[1],))
+
+    @reg("vrvq::bias_grad")
+    def _(grad):
+        return f32(grad, (grad.shape[1],))
+
+    @reg("vrvq::act_backward")
+    def _(y, grad, epilogue):
+        return torch.empty_like(y)
+
+    @reg("vrvq::weight_norm_backward")
+    def _(g, v, dw):
+        return torch.empty_like(g), torch.empty_like(v)
+
+    @reg("vrvq::pack_conv1d_flip")
+    def _(w):
+        cout, cin, k = w.shape
+        return f32(w, (cout, k, round_up(cin, 128)))
+
+    @reg("vrvq::mask_ste")
+    def _(imp, levels, dropout, nq, alpha, n_imps, n_drop):
+        return f32(imp, (imp.shape[0], nq, imp.shape[-1]))
+
+    @reg("vrvq::mask_ste_backward")
+    def _(imp, levels, dmask, alpha, n_imps):
+        return torch.empty_like(imp)
+
+    @reg("vrvq::rvq_encode_train")
+    def _(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, mask):
+        B, D, T = z.shape
+        nq, _n, d = cb.shape
+        return (z.new_empty((B, nq, T), dtype=torch.int64), f32(z, (B, nq * d, T)),
+                f32(z, (B, nq, T)), f32(z, (B, nq, T, d)), f32(z, (B, D, T)))
+
+    @reg("vrvq::rvq_backward")
+    def _(dz_q, g_commit, g_codebook, z, zst, latents, codes, mask, w_in_t, w_out, b_out, mcol,
+          cb):
+        nq, D, d = w_in_t.shape
+        return (torch.empty_like(z), torch.empty_like(mask), f32(z, (nq, d, D)), f32(z, (nq, d)),
+                f32(z, (nq, D, d)), f32(z, (nq, D)), torch.empty_like(cb))
