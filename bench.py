@@ -211,6 +211,47 @@ def build_model(args, dev):
     return model.to(dev).eval(), kwargs
 
 
+TRAIN_CLIP = 16758  # conf/dataset.yml train duration 0.38 s at 44.1 kHz
+
+
+def train_main(args, world: int, rank: int, dev):
+    """configs[3]: the vrvq_a2 training step (scripts/train.py:262-335) with `--batch` clips of
+    0.38 s per rank (global batch 256 at 8 GPUs), DDP over RCCL for the gradient all-reduce."""
+    import vrvq_amd
+    from vrvq_amd.config import A2_KWARGS
+    from vrvq_amd.recipe import load_recipe, synthetic_audio
+    from vrvq_amd.replicas import shard_seed, throughput, timed_steps
+    from vrvq_amd.trainer import LAMBDAS_A2, build_state, train_step
+    model = vrvq_amd.DAC_VRVQ(**A2_KWARGS)
+    load_recipe(model, seed=0)
+    torch.manual_seed(0)
+    state = build_state(model, dev, ddp=world > 1)
+    audio = torch.from_numpy(synthetic_audio(args.batch, TRAIN_CLIP,
+                                             seed=shard_seed(4321, rank))).to(dev)
+
+    def step():
+        return train_step(state, audio, LAMBDAS_A2)
+
+    res_t = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize, device=dev)
+    ms = res_t.seconds / args.steps * 1e3
+    value = throughput(args.batch * TRAIN_CLIP / SR, res_t)
+    losses = {k: round(float(v), 5) for k, v in res_t.last.items()}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "train audio-sec/s (vrvq_a2 generator+discriminator step, 0.38 s clips)",
+            "value": round(value, 3), "unit": "audio-sec/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic uniform audio [-0.5,0.5), recipe random-init weights",
+            "config": {"workload": "vrvq_a2 training step: generator fwd/bwd on the HIP autograd "
+                                   "path, discriminator + mel/stft/GAN losses on PyTorch-ROCm, "
+                                   "AdamW, grad clipping",
+                       "model": "DAC_VRVQ vrvq_a2 (28 cb) + Discriminator",
+                       "global_batch": args.batch * world, "clip_samples": TRAIN_CLIP,
+                       "parallelism": f"dp{world} (DDP, RCCL all-reduce)"},
+            "losses_last_step_rank0": losses}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +261,9 @@ def main():
     ap.add_argument("--n-codebooks", type=int, default=8)
     ap.add_argument("--level", type=float, default=1.0)
     ap.add_argument("--sweep", action="store_true", help="configs[4]: VBR level sweep")
+    ap.add_argument("--train", action="store_true",
+                    help="configs[3]: vrvq_a2 training step (generator + discriminator + losses, "
+                         "DDP over RCCL), 0.38 s clips")
     ap.add_argument("--cpu-clips", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -237,6 +281,12 @@ def main():
     import vrvq_amd
     from vrvq_amd.recipe import synthetic_audio
     from vrvq_amd.replicas import job_rate, shard_seed, throughput, timed_steps
+
+    if args.train:
+        train_main(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     model, kwargs = build_model(args, dev)
     audio = torch.from_numpy(synthetic_audio(args.batch, CLIP_SAMPLES,

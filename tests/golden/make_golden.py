@@ -49,7 +49,8 @@ def install_stubs():
     at.ml = ml
     at.AudioSignal = type("AudioSignal", (), {})
     at.STFTParams = namedtuple("STFTParams", ["window_length", "hop_length", "window_type",
-                                              "match_stride", "padding_type"])
+                                              "match_stride", "padding_type"],
+                                 defaults=(None, None, None, None, None))
     sys.modules["audiotools"] = at
     sys.modules["audiotools.ml"] = ml
     sys.modules["torchmetrics"] = types.ModuleType("torchmetrics")
@@ -326,7 +327,27 @@ def train_fixture(DAC, kw, name, manifest, batch, seed, length=16758, audio_seed
           "rows", manifest[name]["rows"])
 
 
+def discriminator_fixture(ref_root, manifest):
+    """State-dict layout of the reference Discriminator (models/discriminator.py:178-220) and
+    its feature-map shapes for a short input: the training step's discriminator must load
+    reference checkpoints."""
+    from models.discriminator import Discriminator
+    torch.manual_seed(0)
+    d = Discriminator()
+    x = torch.from_numpy(synthetic_audio(1, 4410, seed=99))
+    try:
+        with torch.no_grad():
+            fm = d(x)
+        shapes = [[list(t.shape) for t in f] for f in fm]
+    except Exception as e:  # MRD needs audiotools' STFT (stubbed here): keys only
+        print("discriminator forward unavailable with stubs:", type(e).__name__)
+        shapes = None
+    manifest["discriminator"] = {"state_dict": {k: list(v.shape) for k, v in d.state_dict().items()},
+                                 "fmap_shapes_4410": shapes}
+
+
 def train_all(DAC, ref, manifest):
+    discriminator_fixture(ref, manifest)
     a2 = yml_kwargs(ref, "conf/vrvq/vrvq_a2.yml")
     train_fixture(DAC, a2, "golden_train_a2", manifest, batch=2, seed=2024)
     # all three row kinds of the training quantizer (importance / dropout / full codebook)

@@ -56,3 +56,13 @@ def from_config(path: str, **overrides):
     kw = model_kwargs(load_config(path))
     kw.update(overrides)
     return DAC_VRVQ(**kw)
+
+
+# conf/vrvq/vrvq_a2.yml resolved ($include base_24kbps.yml, training.yml, dataset.yml): the
+# DAC_VRVQ kwargs of the training configuration (BASELINE configs[3]); tests/golden/manifest.json
+# holds the same dict as resolved from the reference's files.
+A2_KWARGS = {"sample_rate": 44100, "encoder_dim": 64, "encoder_rates": [2, 4, 8, 8],
+             "decoder_dim": 1536, "decoder_rates": [8, 8, 4, 2], "n_codebooks": 28,
+             "codebook_size": 1024, "codebook_dim": 8, "quantizer_dropout": 0.0,
+             "model_type": "VBR", "full_codebook_rate": 0.25, "level_min": 0.125,
+             "level_max": 6, "imp2mask_alpha": 2.0}
