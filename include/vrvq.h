@@ -266,6 +266,15 @@ int vrvq_unpack_codes(const uint16_t* packed, const int* counts, const long long
                       int batch, int nq, int frames, int64_t* codes, float* mask,
                       vrvq_stream_t stream);
 
+/* ResidualVectorQuantize.from_latents (models/quantize.py:251-285): per stage i < nq the
+ * nearest normalised codeword of the stage's own latent latents[b][8i..8i+8][t] (decode_latents,
+ * :87-103; the distance expression of vrvq_rvq_chain) -> codes [B][nq][T] int64. latents has
+ * nlat >= 8 nq channels; cbn [nq][ncode][8] / c2 [nq][ncode] from vrvq_codebook_prep. The
+ * z_p rows and z_q follow with vrvq_rvq_gather + vrvq_rvq_expand. */
+int vrvq_rvq_nearest(const float* latents, int batch, int nlat, int frames, int nq,
+                     const float* cbn, const float* c2, int ncode, int cdim, int64_t* codes,
+                     vrvq_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Training step (scripts/train.py:262-330): the backward operators of
  * the generator, used by the torch.autograd.Functions in vrvq_amd/train.py. Every reduction

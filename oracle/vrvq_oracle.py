@@ -205,6 +205,27 @@ class Oracle:
             z_q = masked_sum(z_q_is, mask)
         return z_q, np.concatenate(z_p, axis=1), z_q_is
 
+    # models/quantize.py:251-285 (ResidualVectorQuantize.from_latents): per whole stage of the
+    # latents, decode_latents (:87-103) on the stage's own slice (no residual), out_proj, sum.
+    def from_latents(self, latents):
+        B, C, T = latents.shape
+        n = min(C // 8, self.n_codebooks)
+        z_q = np.zeros((B, self.sd["quantizer.quantizers.0.out_proj.bias"].shape[0], T), F32)
+        z_p, codes = [], []
+        for i in range(n):
+            p = f"quantizer.quantizers.{i}"
+            enc = latents[:, 8 * i: 8 * i + 8].transpose(0, 2, 1).reshape(-1, 8)
+            cb = self.sd[p + ".codebook.weight"]
+            en = enc / np.maximum(np.sqrt(np.sum(enc * enc, 1, keepdims=True)), F32(1e-12))
+            cn = cb / np.maximum(np.sqrt(np.sum(cb * cb, 1, keepdims=True)), F32(1e-12))
+            dist = (np.sum(en * en, 1, keepdims=True) - 2 * en @ cn.T) + np.sum(cn * cn, 1, keepdims=True).T
+            idx = np.argmax(-dist, axis=1).reshape(B, T)
+            zp = cb[idx].transpose(0, 2, 1).astype(F32)
+            z_p.append(zp)
+            codes.append(idx.astype(np.int64))
+            z_q = z_q + self.conv(zp, p + ".out_proj")
+        return z_q, np.concatenate(z_p, axis=1), np.stack(codes, axis=1)
+
     # models/quantize.py:328-443 (eval) and :136-214 (CBR eval)
     def quantize(self, z, n_quantizers=None, feat=None, level=1.0):
         nq = self.n_codebooks

@@ -237,7 +237,29 @@ def mask_kat(ref_utils, manifest):
     manifest["mask_kat"] = {"s": [float(v) for v in s.reshape(-1)], "results": out}
 
 
+def from_latents_fixture(DAC, kw, name, manifest, batch=2, frames=40, seed=21):
+    """ResidualVectorQuantize.from_latents (models/quantize.py:251-285) of the reference on
+    random latents: all 8 stages, and a 43-channel input (5 whole stages, 3 channels ignored)."""
+    model = build(DAC, kw)
+    q = model.quantizer
+    g = torch.Generator().manual_seed(seed)
+    res = {}
+    for tag, ch in (("full", 8 * len(q.quantizers)), ("part", 43)):
+        lat = torch.randn(batch, ch, frames, generator=g) * 0.7
+        with torch.no_grad():
+            z_q, z_p, codes = q.from_latents(lat)
+        res.update({f"{tag}_latents": lat.numpy(), f"{tag}_z_q": z_q.numpy(),
+                    f"{tag}_z_p": z_p.numpy(), f"{tag}_codes": codes.numpy()})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+    manifest[name] = {"kwargs": kw, "batch": batch, "frames": frames, "latents_seed": seed,
+                      "weight_seed": 0,
+                      "state_dict": {k: list(v.shape) for k, v in model.state_dict().items()}}
+    print(name, "codes", res["full_codes"].shape, res["part_codes"].shape)
+
+
 def from_codes_all(DAC, ref, manifest):
+    from_latents_fixture(DAC, yml_kwargs(ref, "conf/original_dac/cbr.yml"), "golden_from_latents_cbr",
+                         manifest)
     from_codes_fixture(DAC, yml_kwargs(ref, "conf/original_dac/cbr.yml"), "golden_from_codes_cbr",
                        manifest)
     from_codes_fixture(DAC, yml_kwargs(ref, "conf/base.yml"), "golden_from_codes_vbr", manifest,

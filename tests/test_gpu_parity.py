@@ -645,3 +645,16 @@ def test_pack_roundtrip_full_batch_and_file(manifest, tmp_path):
     with torch.no_grad():
         z_q, _, _ = model.quantizer.from_codes(codes, mask_imp=mask)
     assert rel_err(z_q.cpu().numpy(), enc["z_q"].cpu().numpy()) < TOL
+
+
+@pytest.mark.parametrize("tag", ["full", "part"])
+def test_from_latents_vs_reference(manifest, tag):
+    """ResidualVectorQuantize.from_latents (models/quantize.py:251-285) on the HIP path against
+    the reference's own outputs: codes and raw rows bit-exact, z_q within 1e-4."""
+    g = load_golden("golden_from_latents_cbr")
+    model = model_for(manifest, "golden_from_latents_cbr")
+    with torch.no_grad():
+        z_q, z_p, codes = model.quantizer.from_latents(t(g[f"{tag}_latents"]))
+    np.testing.assert_array_equal(codes.cpu().numpy(), g[f"{tag}_codes"])
+    np.testing.assert_array_equal(z_p.cpu().numpy(), g[f"{tag}_z_p"])
+    assert rel_err(z_q.cpu().numpy(), g[f"{tag}_z_q"]) < TOL

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--res", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--convt", type=int, default=0, help="transposed conv with this stride")
+    ap.add_argument("--ru", action="store_true",
+                    help="fused ResidualUnit (k7 dil --dil, k1, skip) with cin channels")
     ap.add_argument("--snake-in", action="store_true", help="Snake on load (consumer side)")
     ap.add_argument("--no-snake-out", action="store_true", help="no producer-side Snake output")
     args = ap.parse_args()
@@ -36,7 +38,19 @@ def main():
     a_in, i_in = (alpha, inv) if args.snake_in else (None, None)
     ao = (torch.rand(args.cout, generator=g) + 0.5).to(dev)
     osn = None if args.no_snake_out else (ao, ops.snake_inv_alpha(ao))
-    if args.convt:
+    if args.ru:
+        C = args.cin
+        w7 = (torch.randn(C, C, 7, generator=g) * 0.02).to(dev)
+        w1 = (torch.randn(C, C, 1, generator=g) * 0.02).to(dev)
+        wp7, cp = ops.pack_conv1d_weight(w7)
+        wp1, _ = ops.pack_conv1d_weight(w1)
+        b = torch.zeros(C, device=dev)
+        x_snk = x.clone()  # snake1(x) in the model; any values time the same
+        osn = (ao[:C].contiguous(), ops.snake_inv_alpha(ao[:C].contiguous()))
+        fn = lambda: ops.residual_unit(x, x_snk, args.dil, wp7, b, alpha, inv, wp1, b, cp,
+                                       out_snake=osn, want_raw=True)
+        flops = 2.0 * args.batch * C * C * 8 * args.t
+    elif args.convt:
         w = (torch.randn(args.cin, args.cout, 2 * args.convt, generator=g) * 0.02).to(dev)
         wp, cp = ops.pack_convt1d_weight(w, args.convt)
         b = torch.zeros(args.cout, device=dev)

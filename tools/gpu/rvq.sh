@@ -8,7 +8,7 @@ run() { local name=$1 to=$2; shift 2
   echo "=== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1; local rc=$?
   echo "=== $name rc=$rc"; grep -v amdgpu.ids "gpurun_out/${TAG}_$name.log" | tail -${TAIL:-6}
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; return 0; }
-run pytest_rvq 300 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread -k "rvq or golden or model_forward or from_codes or config or sweep or smoke"
+run pytest_rvq 300 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread -k "rvq or golden or model_forward or from_codes or from_latents or config or sweep or smoke or graph"
 run bench_b32 120 python tools/rvq_bench.py --batch 32 --nq 8
 run bench_b64 120 python tools/rvq_bench.py --batch 64 --nq 32
 run bench_b64n28 120 python tools/rvq_bench.py --batch 64 --nq 28

@@ -48,6 +48,7 @@ SIGNATURES = {
     "vrvq_pack_codes": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "vrvq_unpack_offsets": [_P, _I, _I, _P, _P, _P],
     "vrvq_unpack_codes": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "vrvq_rvq_nearest": [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P],
     # training step
     "vrvq_wgrad_plan": [_I, _I, _I, _I, _I, _P, _P],
     "vrvq_conv1d_wgrad": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P,

@@ -173,7 +173,78 @@ __global__ __launch_bounds__(256) void rvq_gather_kernel(const int64_t* __restri
   }
 }
 
+// Nearest normalised codeword of each stage's own latent (ResidualVectorQuantize.from_latents,
+// models/quantize.py:251-285 via decode_latents :87-103): no residual chain, so every
+// (clip, stage, frame) is independent. Workgroup = (stage, 256 frames) with the stage's
+// normalised codebook and squared norms in LDS (read as broadcasts); the distance is the chain
+// kernel's expression: e = z / max(||z||, 1e-12) with pairwise sums, dot in k order,
+// fma(dot, -2, sum e^2) + c2, lowest index on ties.
+__global__ __launch_bounds__(256) void rvq_nearest_kernel(const float* __restrict__ latents,
+                                                          int batch, int nlat, int frames,
+                                                          const float* __restrict__ cbn,
+                                                          const float* __restrict__ c2, int ncode,
+                                                          int64_t* __restrict__ codes, int nq) {
+  extern __shared__ float nsm[];  // [ncode][8] codebook, [ncode] c2
+  const int i = blockIdx.y;
+  float* cb_s = nsm;
+  float* c2_s = nsm + ncode * 8;
+  for (int e = threadIdx.x; e < ncode * 8; e += 256) cb_s[e] = cbn[(size_t)i * ncode * 8 + e];
+  for (int e = threadIdx.x; e < ncode; e += 256) c2_s[e] = c2[(size_t)i * ncode + e];
+  __syncthreads();
+  const long long n = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (n >= (long long)batch * frames) return;
+  const int b = (int)(n / frames), t = (int)(n - (long long)b * frames);
+  float z[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    z[k] = latents[((size_t)b * nlat + (size_t)i * 8 + k) * frames + t];
+    q[k] = z[k] * z[k];
+  }
+  const float n2 = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  const float nrm = fmaxf(sqrtf(n2), 1e-12f);
+  float e[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    e[k] = z[k] / nrm;
+    q[k] = e[k] * e[k];
+  }
+  const float e2 = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  float best = INFINITY;
+  int bi = 0;
+  for (int c = 0; c < ncode; ++c) {
+    const float* r = cb_s + c * 8;
+    float d = r[0] * e[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) d = fmaf(r[k], e[k], d);
+    const float dist = fmaf(d, -2.0f, e2) + c2_s[c];
+    if (dist < best) {  // increasing code index: strict < keeps the first
+      best = dist;
+      bi = c;
+    }
+  }
+  codes[((size_t)b * nq + i) * frames + t] = bi;
+}
+
 }  // namespace
+
+extern "C" int vrvq_rvq_nearest(const float* latents, int batch, int nlat, int frames, int nq,
+                                const float* cbn, const float* c2, int ncode, int cdim,
+                                int64_t* codes, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(latents && cbn && c2 && codes && batch > 0 && frames > 0 && nq > 0);
+  VRVQ_CHECK_ARG(ncode > 0 && nlat >= nq * 8);
+  if (cdim != 8 || ncode > 4096) return VRVQ_ERR_UNSUPPORTED;
+  const long long nf = (long long)batch * frames;
+  VRVQ_CHECK_ARG((nf + 255) / 256 < 0x7fffffffLL);
+  const size_t lds = (size_t)ncode * 9 * sizeof(float);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_nearest_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(rvq_nearest_kernel, dim3((unsigned)((nf + 255) / 256), nq), dim3(256), lds,
+                     as_stream(stream), latents, batch, nlat, frames, cbn, c2, ncode, codes, nq);
+  return vrvq_launch_status();
+}
 
 extern "C" const char* vrvq_status_string(int status) {
   switch (status) {

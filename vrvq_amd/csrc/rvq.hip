@@ -107,12 +107,15 @@ __global__ void rvq_frag_kernel(const float* __restrict__ cbn, int nq, int N,
 // Projection: part[s][n][r] = sum_{c in split s} W_in_t[r/8][c][r%8] z[b][c][t], n = b*T + t,
 // r < R = nq*8. Workgroup = (clip b, frame tile of <= 96, channel split s, 64-row block), 8
 // waves: wave w computes rows 16 (w & 3) .. +15 for column tiles 3 (w >> 2) .. +2 with
-// v_mfma_f32_16x16x4_f32. K = 128 channels in 4 chunks of 32, double-buffered in LDS: the
-// [32 ch][96 t] slab of z (row segments of one clip, coalesced) and the [32][64] weight block
-// of chunk c+1 are loaded into registers while the MFMAs consume chunk c. Output: lane l holds
-// 4 consecutive rows of one frame -> one float4 store.
+// v_mfma_f32_16x16x4_f32. All of the workgroup's loads (the [128 ch][96 t] slab of z: row
+// segments of one clip, and its [128][64] weight block) are issued up front, in 4 K chunks of
+// 32 channels, each chunk to its own LDS buffer: chunk c is stored (waiting only for its own
+// loads — they complete in issue order) and consumed by the MFMAs while chunks c+1.. are still
+// landing. One HBM round trip per workgroup instead of one per chunk. Output: lane l holds 4
+// consecutive rows of one frame -> one float4 store.
 constexpr int PJ_NT = 512;
 constexpr int PJ_KC = 32;                       // channels per K chunk
+constexpr int PJ_NC = PJ_CPS / PJ_KC;           // chunks (4)
 constexpr int PJ_ZQ = PJ_KC * PJ_TC / PJ_NT;    // z loads per thread per chunk (6)
 constexpr int PJ_STG = PJ_KC * PJ_ZLD + PJ_KC * PJ_WLD;
 
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
                                                             int nq, int n_tc,
                                                             const float* __restrict__ w_in_t,
                                                             float* __restrict__ part, int NF) {
-  __shared__ __attribute__((aligned(16))) float sm[2 * PJ_STG];
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // PJ_NC * PJ_STG floats
   const int tc = blockIdx.x % n_tc, b = blockIdx.x / n_tc;
   const int s = blockIdx.y, rb = blockIdx.z;
   const int R = nq * RCD;
@@ -129,47 +132,39 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
-  float zv[PJ_ZQ];
-  float4 wv;
-  auto load = [&](int kc) {  // chunk kc -> registers
+  float zv[PJ_NC][PJ_ZQ];
+  float4 wv[PJ_NC];
+  const int sl = tid >> 6, rem = tid & 63;
+  const int st = rb * 8 + sl;
+#pragma unroll
+  for (int kc = 0; kc < PJ_NC; ++kc) {  // every load of the workgroup in flight at once
 #pragma unroll
     for (int q = 0; q < PJ_ZQ; ++q) {
       const int e = tid + PJ_NT * q;
       const int c = e / PJ_TC, t = e - c * PJ_TC;
-      zv[q] = t < ntl ? zb[(size_t)(kc * PJ_KC + c) * T + t] : 0.0f;
+      zv[kc][q] = t < ntl ? zb[(size_t)(kc * PJ_KC + c) * T + t] : 0.0f;
     }
     // 8 stages x 32 channels x 2 float4 = one float4 per thread
-    const int sl = tid >> 6, rem = tid & 63;
-    const int st = rb * 8 + sl;
-    wv = st < nq ? ld4(w_in_t + ((size_t)st * RD + s * PJ_CPS + kc * PJ_KC) * RCD + rem * 4)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  auto store = [&](float* stg) {
-    float* z_s = stg;
-    float* w_s = stg + PJ_KC * PJ_ZLD;
-#pragma unroll
-    for (int q = 0; q < PJ_ZQ; ++q) {
-      const int e = tid + PJ_NT * q;
-      const int c = e / PJ_TC, t = e - c * PJ_TC;
-      z_s[c * PJ_ZLD + t] = zv[q];
-    }
-    const int sl = tid >> 6, rem = tid & 63;
-    *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) = wv;
-  };
+    wv[kc] = st < nq ? ld4(w_in_t + ((size_t)st * RD + s * PJ_CPS + kc * PJ_KC) * RCD + rem * 4)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const int rt = wave & 3, cg = wave >> 2;
   const int lr = lane & 15, lk = lane >> 4;
   f32x4 acc[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  load(0);
-  store(sm);
-  __syncthreads();
-#pragma unroll 1
-  for (int kc = 0; kc < PJ_CPS / PJ_KC; ++kc) {
-    const bool more = kc + 1 < PJ_CPS / PJ_KC;
-    if (more) load(kc + 1);  // in flight during the MFMAs below
-    const float* z_s = sm + (kc & 1) * PJ_STG;
-    const float* w_s = z_s + PJ_KC * PJ_ZLD;
+#pragma unroll
+  for (int kc = 0; kc < PJ_NC; ++kc) {
+    float* z_s = sm + kc * PJ_STG;
+    float* w_s = z_s + PJ_KC * PJ_ZLD;
+#pragma unroll
+    for (int q = 0; q < PJ_ZQ; ++q) {
+      const int e = tid + PJ_NT * q;
+      const int c = e / PJ_TC, t = e - c * PJ_TC;
+      z_s[c * PJ_ZLD + t] = zv[kc][q];
+    }
+    *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) = wv[kc];
+    __syncthreads();
     // all column tiles unconditionally (zero-padded frames): a runtime-guarded MFMA makes the
     // compiler shuffle the accumulators through v_mov / accvgpr copies every step
 #pragma unroll
@@ -182,11 +177,8 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
       }
     }
-    if (more) store(sm + ((kc + 1) & 1) * PJ_STG);
-    __syncthreads();
   }
   const int r0 = rb * 64 + rt * 16;
-  if (r0 >= R) return;
   // D layout: lane l, reg q -> row 4*(l>>4) + q of the wave's 16, column (frame) l & 15
   const int rr = r0 + 4 * lk;  // R = 8 nq: rows rr..rr+3 are all valid iff rr < R
   if (rr >= R) return;
@@ -205,8 +197,9 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
 // The chain. Workgroup = frames [n0, n0 + nf) of the flattened (b, t) axis, nf <= 16; 8 waves.
 //
 // Stage i, S1 (all waves):
-//   - deferred U updates: pu[f][ip] -= M_{ip,i-1} zst_{i-1} for ip > i (spread over all threads;
-//     ip = i was done on the critical path in S2 of stage i-1);
+//   - deferred U updates: pu[f][ip] -= M_{ip,i-1} zst_{i-1} for ip > i (spread over all threads,
+//     issued after the candidate-row gather so they run under its L2 latency; ip = i was done on
+//     the critical path in S2 of stage i-1);
 //   - distance scan on the matrix cores: wave w owns codes [w N/8, (w+1) N/8) as 16-code tiles;
 //     D[code][frame] = cbn . e by two v_mfma_f32_16x16x4_f32 per tile (k = 0..3, then 4..7 on
 //     the same accumulator: the k-ordered fma chain of the reference's dot, bitwise), then per
@@ -380,7 +373,11 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
       if (i + 1 < nq && tid * 4 < R * RCD)
         reinterpret_cast<float4*>(m_s + (i % 3) * R * RCD)[tid] = mn;
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the c2 slice is in LDS for the scan
-      // deferred U updates from stage i-1 for targets ip > i
+    }
+    // deferred U updates from stage i-1 for targets ip > i (needed from S2 of this stage on):
+    // run after the scan has issued its candidate-row gather, under that L2 latency
+    auto deferred_updates = [&]() {
+      if (i == 0) return;
       const int nip = nq - 1 - i;
       const float* mj = m_s + ((i - 1) % 3) * R * RCD;
       for (int e = tid; e < nf * nip * RCD; e += CH_NT) {
@@ -391,7 +388,7 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
         float* pp = pu_s + (f * nq + ip) * RCD + k;
         *pp = *pp - dot8(ld4(mr), ld4(mr + 4), ld4(zr), ld4(zr + 4));
       }
-    }
+    };
     CSTAMP(i, 1);
     float an[NT][2];
     CSTAMP(i, 2);
@@ -453,6 +450,7 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
         if (i + 2 < nq && tid * 4 < R * RCD)  // M_{.,i+1}: needed from stage i+1 on
           mn = ld4(a.mcol + (size_t)(i + 1) * R * RCD + tid * 4);
       }
+      deferred_updates();
       if (lane < nf) {
         cd_s[lane * CH_NW + wave] = best;
         ci_s[lane * CH_NW + wave] = bidx;
@@ -646,7 +644,15 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
   VRVQ_CHECK_ARG(nf * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
   const int n_tc = (frames + PJ_TC - 1) / PJ_TC;
   const dim3 grid((unsigned)(batch * n_tc), PJ_SPLIT, (unsigned)((nq + 7) / 8));
-  hipLaunchKernelGGL(rvq_project_kernel, grid, dim3(PJ_NT), 0, st, z, frames, nq, n_tc, w_in_t,
+  const int lds = PJ_NC * PJ_STG * (int)sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_project_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(rvq_project_kernel, grid, dim3(PJ_NT), lds, st, z, frames, nq, n_tc, w_in_t,
                      part, (int)nf);
   return vrvq_launch_status();
 }

@@ -366,6 +366,24 @@ std::tuple<Tensor, Tensor, Tensor> rvq_gather(const Tensor& codes, const Tensor&
   return {zst, z_p, err};
 }
 
+// decode_latents of every stage (models/quantize.py:87-103) for from_latents (:251-285).
+Tensor rvq_nearest(const Tensor& latents, const Tensor& cbn, const Tensor& c2, int64_t nq) {
+  check_t(latents, "latents");
+  check_on(cbn, latents, "cbn");
+  check_on(c2, latents, "c2");
+  TORCH_CHECK(latents.dim() == 3, "from_latents: latents must be (B, N*d, T)");
+  TORCH_CHECK(cbn.dim() == 3 && cbn.size(0) >= nq && c2.numel() == cbn.size(0) * cbn.size(1),
+              "rvq_nearest: cbn (nq, N, d) / c2 (nq, N)");
+  c10::DeviceGuard guard(latents.device());
+  const int64_t B = latents.size(0), C = latents.size(1), T = latents.size(2);
+  Tensor codes = at::empty({B, nq, T}, latents.options().dtype(at::kLong));
+  check_rc(vrvq_rvq_nearest(latents.data_ptr<float>(), (int)B, (int)C, (int)T, (int)nq,
+                            cbn.data_ptr<float>(), c2.data_ptr<float>(), (int)cbn.size(1),
+                            (int)cbn.size(2), codes.data_ptr<int64_t>(), stream_of(latents)),
+           "vrvq_rvq_nearest");
+  return codes;
+}
+
 // out_proj of every stage from straight-through / codebook rows + (masked) sum
 // (models/quantize.py:77, 217-249; scripts/inference.py:99-100).
 std::tuple<Tensor, Tensor, Tensor> rvq_expand(const Tensor& zst, const Tensor& w_out,
@@ -815,6 +833,7 @@ TORCH_LIBRARY(vrvq, m) {
       "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
       "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("rvq_gather(Tensor codes, Tensor cb) -> (Tensor, Tensor, Tensor)");
+  m.def("rvq_nearest(Tensor latents, Tensor cbn, Tensor c2, int nq) -> Tensor");
   m.def(
       "rvq_expand(Tensor zst, Tensor w_out, Tensor b_out, Tensor? imp, float level, "
       "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor)");
@@ -870,6 +889,7 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("rvq_frag", &rvq_frag); \
   m.impl("rvq_encode", &rvq_encode); \
   m.impl("rvq_gather", &rvq_gather); \
+  m.impl("rvq_nearest", &rvq_nearest); \
   m.impl("rvq_expand", &rvq_expand); \
   m.impl("masked_loss", &masked_loss); \
   m.impl("scale_imp", &scale_imp); \

@@ -235,7 +235,23 @@ class ResidualVectorQuantize(nn.Module):
         return z_q, z_p, codes
 
     def from_latents(self, latents: torch.Tensor):
-        raise NotImplementedError("from_latents is outside the hot path (SURVEY.md §8f)")
+        """Unquantised latents -> (z_q, z_p, codes) (models/quantize.py:251-285): the stages
+        whose 8 channels fit in latents.shape[1] each pick the nearest normalised codeword of
+        their own slice (decode_latents, no residual chain: vrvq_rvq_nearest), then the raw
+        rows (rvq_gather) go through out_proj and are summed (rvq_expand)."""
+        if not isinstance(latents, torch.Tensor) or latents.dim() != 3:
+            raise RuntimeError("from_latents: latents must be a (B, N*d, T) tensor")
+        dims = np.cumsum([0] + [self.quantizers[0].codebook_dim] * self.n_codebooks)
+        n = int(np.where(dims <= latents.shape[1])[0].max())
+        if n == 0:  # the reference's torch.cat of an empty list
+            raise RuntimeError("from_latents: fewer channels than one codebook_dim")
+        st = self.stacked()
+        lat = latents.contiguous()
+        codes = ops.rvq_nearest(lat, st.cbn, st.c2, n)
+        zst, z_p = ops.rvq_gather(codes, st.cb, check=False)
+        _, z_q, _ = ops.rvq_expand(zst, st.w_out[:n], st.b_out[:n], None, 1.0,
+                                   want_z_q_is=False, want_mask=False)
+        return z_q, z_p, codes
 
 
 class VBRResidualVectorQuantize(ResidualVectorQuantize):

@@ -177,6 +177,12 @@ def rvq_gather(codes: torch.Tensor, cb: torch.Tensor, check: bool = True):
     return zst, z_p
 
 
+def rvq_nearest(latents, cbn, c2, nq: int) -> torch.Tensor:
+    """decode_latents of stages 0..nq-1 on their own latents (from_latents): codes int64
+    [B, nq, T]."""
+    return _ops().rvq_nearest(latents, cbn, c2, int(nq))
+
+
 def rvq_expand(zst, w_out, b_out, imp=None, level: float = 1.0, want_z_q_is: bool = True,
                want_mask: bool = True):
     """z_q_is / masked z_q / mask from the straight-through vectors (HBM-streaming kernel)."""
@@ -344,6 +350,10 @@ def _register_fakes():
         d = cb.shape[2]
         return (f32(cb, (B, nq, T, d)), f32(cb, (B, nq * d, T)),
                 codes.new_empty((1,), dtype=torch.int32))
+
+    @reg("vrvq::rvq_nearest")
+    def _(latents, cbn, c2, nq):
+        return latents.new_empty((latents.shape[0], nq, latents.shape[2]), dtype=torch.int64)
 
     @reg("vrvq::rvq_expand")
     def _(zst, w_out, b_out, imp, level, want_z_q_is, want_mask):
