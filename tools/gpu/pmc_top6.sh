@@ -31,6 +31,6 @@ done
 j=0
 for P in "$P1" "$P2"; do
   j=$((j+1))
-  run rvqp${j} 90 rocprofv3 --pmc $P --kernel-include-regex "rvq_" -d gpurun_out/pmc6/rvqp${j} -o run --output-format csv -- python tools/rvq_bench.py --iters 5
+  run rvqp${j} 90 rocprofv3 --pmc $P --kernel-include-regex "rvq_" -d gpurun_out/pmc6/rvqp${j} -o run --output-format csv -- python tools/rvq_bench.py --iters 8
 done
 exit 0

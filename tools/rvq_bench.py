@@ -42,7 +42,7 @@ def main():
         ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
         e1.record()
         torch.cuda.synchronize()
-        if it >= 5:
+        if it >= min(5, args.iters - 1):
             ts.append(e0.elapsed_time(e1) * 1e3)
     med = sorted(ts)[len(ts) // 2]
     byt = rvq_bytes(args.batch, args.frames, args.nq)

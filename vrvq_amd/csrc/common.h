@@ -18,11 +18,32 @@ static inline int vrvq_launch_status() {
 
 static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// sin(u)^2 for Snake: Cody-Waite reduction of u by pi (three-term pi, exact with fma for
+// |u| < 2^20), then the odd Taylor polynomial of sin to degree 13 on |r| <= pi/2 (truncation
+// < 7e-10). sin(u)^2 = sin(r)^2, so the quadrant sign is not needed. 14 VALU instead of the
+// ~40 of the general sinf (the mul of the reference's alpha * x is kept as is); max abs error
+// of the square 2.2e-7 (sinf: 1e-7) — within the parity tolerance, and the Snake-heavy
+// residual units spend most of their VALU here.
+__device__ __forceinline__ float sin_sq(float u) {
+  const float k = rintf(u * 0.318309886183790672f);
+  float r = fmaf(-k, 3.14159274101257324e+00f, u);
+  r = fmaf(-k, -8.74227765734758577e-08f, r);
+  r = fmaf(-k, -3.43061790e-15f, r);
+  const float r2 = r * r;
+  float p = 1.6059043836821614e-10f;            //  1/13!
+  p = fmaf(p, r2, -2.5052108385441720e-08f);    // -1/11!
+  p = fmaf(p, r2, 2.7557319223985893e-06f);     //  1/9!
+  p = fmaf(p, r2, -1.9841269841269841e-04f);    // -1/7!
+  p = fmaf(p, r2, 8.3333333333333333e-03f);     //  1/5!
+  p = fmaf(p, r2, -1.6666666666666667e-01f);    // -1/3!
+  const float s = fmaf(r * r2, p, r);
+  return s * s;
+}
+
 // Snake activation, models/layers.py:30: x + (alpha + 1e-9)^-1 * sin(alpha * x)^2.
-// Evaluated as the reference's op sequence (mul, sin, square, mul, add), one rounding each.
+// The reference's op sequence (mul, sin, square, mul, add); sin^2 from sin_sq.
 __device__ __forceinline__ float snake_act(float v, float alpha, float inv_alpha) {
-  const float s = sinf(alpha * v);
-  return v + inv_alpha * (s * s);
+  return v + inv_alpha * sin_sq(alpha * v);
 }
 
 // 8-term dot product in k order (fmaf chain); used for in_proj/out_proj/codebook distance.

@@ -349,6 +349,18 @@ class CodecMixin:
     def _conv_layers(self):
         return [m for m in self.modules() if isinstance(m, (WNConv1d, WNConvTranspose1d))]
 
+    @torch.no_grad()
+    def compress(self, audio_path_or_signal, win_duration: float = 1.0, verbose: bool = False,
+                 normalize_db: float = -16, n_quantizers: int = None):
+        """models/dac_base.py:130-240 — raises NotImplementedError in the reference (:161)
+        before any work; kept identical for drop-in behaviour."""
+        raise NotImplementedError
+
+    @torch.no_grad()
+    def decompress(self, obj, verbose: bool = False):
+        """models/dac_base.py:243-304 — raises NotImplementedError in the reference (:264)."""
+        raise NotImplementedError
+
     def get_delay(self):
         l_out = self.get_output_length(0)
         L = l_out
