@@ -306,9 +306,11 @@ int vrvq_snake_backward(const float* x, const float* alpha, const float* inv_alp
                         float* dalpha, float* workspace, long long workspace_bytes,
                         vrvq_stream_t stream);
 
-/* Conv bias gradient: db[c] = sum_{b,t} grad[b][c][t]. */
+/* Conv bias gradient: db[c] = sum_{b,t} grad[b][c][t] (per-(clip, chunk) partials in the
+ * workspace, summed in a fixed order). */
+int vrvq_bias_grad_workspace(int batch, int channels, int frames, long long* bytes);
 int vrvq_bias_grad(const float* grad, int batch, int channels, int frames, float* db,
-                   vrvq_stream_t stream);
+                   float* workspace, long long workspace_bytes, vrvq_stream_t stream);
 
 /* Tanh (models/dac_vrvq.py:74) / Sigmoid (models/importance_subnet.py:44) backward from the
  * saved output y: out = g (1 - y^2) | g y (1 - y). */

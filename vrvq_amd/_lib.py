@@ -55,7 +55,8 @@ SIGNATURES = {
                           ctypes.c_longlong, _P, _P],
     "vrvq_snake_backward_workspace": [_I, _I, _I, _P],
     "vrvq_snake_backward": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, ctypes.c_longlong, _P],
-    "vrvq_bias_grad": [_P, _I, _I, _I, _P, _P],
+    "vrvq_bias_grad_workspace": [_I, _I, _I, _P],
+    "vrvq_bias_grad": [_P, _I, _I, _I, _P, _P, ctypes.c_longlong, _P],
     "vrvq_act_backward": [_P, _P, ctypes.c_longlong, _I, _P, _P],
     "vrvq_weight_norm_backward": [_P, _P, _P, _I, _I, _P, _P, _P],
     "vrvq_pack_conv1d_flip": [_P, _I, _I, _I, _I, _P, _P],

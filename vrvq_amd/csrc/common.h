@@ -40,6 +40,32 @@ __device__ __forceinline__ float sin_sq(float u) {
   return s * s;
 }
 
+// sin(r) and cos(r) of the reduced argument of u (r = u - k pi, |r| <= pi/2): sin(u) cos(u) =
+// sin(r) cos(r) and sin(u)^2 = sin(r)^2 (the (-1)^k signs cancel) -- what Snake's backward
+// needs. Same reduction as sin_sq; Taylor polynomials to degree 13 / 14.
+__device__ __forceinline__ void sincos_reduced(float u, float* sr, float* cr) {
+  const float k = rintf(u * 0.318309886183790672f);
+  float r = fmaf(-k, 3.14159274101257324e+00f, u);
+  r = fmaf(-k, -8.74227765734758577e-08f, r);
+  r = fmaf(-k, -3.43061790e-15f, r);
+  const float r2 = r * r;
+  float p = 1.6059043836821614e-10f;
+  p = fmaf(p, r2, -2.5052108385441720e-08f);
+  p = fmaf(p, r2, 2.7557319223985893e-06f);
+  p = fmaf(p, r2, -1.9841269841269841e-04f);
+  p = fmaf(p, r2, 8.3333333333333333e-03f);
+  p = fmaf(p, r2, -1.6666666666666667e-01f);
+  *sr = fmaf(r * r2, p, r);
+  float q = -1.1470745597729725e-11f;           // -1/14!
+  q = fmaf(q, r2, 2.0876756987868099e-09f);     //  1/12!
+  q = fmaf(q, r2, -2.7557319223985891e-07f);    // -1/10!
+  q = fmaf(q, r2, 2.4801587301587302e-05f);     //  1/8!
+  q = fmaf(q, r2, -1.3888888888888889e-03f);    // -1/6!
+  q = fmaf(q, r2, 4.1666666666666667e-02f);     //  1/4!
+  q = fmaf(q, r2, -0.5f);                       // -1/2!
+  *cr = fmaf(q, r2, 1.0f);
+}
+
 // Snake activation, models/layers.py:30: x + (alpha + 1e-9)^-1 * sin(alpha * x)^2.
 // The reference's op sequence (mul, sin, square, mul, add); sin^2 from sin_sq.
 __device__ __forceinline__ float snake_act(float v, float alpha, float inv_alpha) {

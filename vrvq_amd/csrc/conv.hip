@@ -215,7 +215,11 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     const long long blocks96 = (long long)((a.M + 127) / 128) * batch;
     bn = blocks96 >= 384 ? 96 : 32;
   }
-  else if (a.ng < 4096 && conv_bn_rule() == 0 && waste(64) * 10 < waste(128) * 7) bn = 64;
+  // k = 16 (the stride-8 encoder convs): the 8 MB weight block does not fit in L2, so the
+  // 128-wide tile's halved weight re-streaming beats its padding (1490 -> 1323 us at T = 696,
+  // profiles/r02u_conv_ab.txt)
+  else if (a.ng < 4096 && KS != 16 && conv_bn_rule() == 0 && waste(64) * 10 < waste(128) * 7)
+    bn = 64;
   else if (a.ng < 4096 && conv_bn_rule() == 1 && waste(128) * 100 > a.ng * 15) bn = 64;
   else bn = 128;
   if (KS == 2 && a.up > 0 && 128 % a.up != 0) {

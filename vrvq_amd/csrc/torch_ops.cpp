@@ -625,8 +625,14 @@ Tensor bias_grad(const Tensor& grad) {
   TORCH_CHECK(grad.dim() == 3, "bias_grad: grad must be (B, C, T)");
   c10::DeviceGuard guard(grad.device());
   Tensor db = empty_f({grad.size(1)}, grad);
+  long long bytes = 0;
+  check_rc(vrvq_bias_grad_workspace((int)grad.size(0), (int)grad.size(1), (int)grad.size(2),
+                                    &bytes),
+           "vrvq_bias_grad_workspace");
+  Tensor ws = empty_f({(bytes + 3) / 4}, grad);
   check_rc(vrvq_bias_grad(grad.data_ptr<float>(), (int)grad.size(0), (int)grad.size(1),
-                          (int)grad.size(2), db.data_ptr<float>(), stream_of(grad)),
+                          (int)grad.size(2), db.data_ptr<float>(), ws.data_ptr<float>(),
+                          (long long)ws.numel() * 4, stream_of(grad)),
            "vrvq_bias_grad");
   return db;
 }

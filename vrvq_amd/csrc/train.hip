@@ -22,7 +22,8 @@ namespace {
 //                  (y[co][t s - p + k] += W[ci][co][k] xs[ci][t])
 // Workgroup = (64 m x 64 c tile, tap k, split); 4 waves of 32 x 32; K_red chunks of 32
 // (b, t) values staged in LDS; partial[split][m][c][k] reduced in split order afterwards.
-constexpr int WG_BM = 64, WG_BN = 64, WG_KT = 32;
+constexpr int WG_BM = 64, WG_BN = 64;
+constexpr int WG_WMAX = 192;           // X-window samples per staged row
 
 struct WgradArgs {
   const float* A; int M, TA;
@@ -30,67 +31,95 @@ struct WgradArgs {
   const float* alpha_a; const float* inv_alpha_a;
   const float* alpha; const float* inv_alpha;
   int B, K, s, p, d;
-  int n_split, chunks;   // total (b, t-chunk) chunks, split evenly over n_split
+  int n_split, chunks;   // (clip, time chunk) units, split evenly over n_split
+  int kt_sh, W, WP, n_kg;  // log2 time chunk, window, padded row stride (odd), tap groups
   float* part;           // [n_split][M][C][K]
 };
 
-__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
-  __shared__ float A_s[WG_BM][WG_KT + 1];
-  __shared__ float X_s[WG_BN][WG_KT + 1];
+// Workgroup = (64 m x 64 c tile, group of KG taps, split). Per (clip, KT-sample) chunk the
+// A rows [64][KT] and the X window [64 channels][(KT-1) s + (KG-1) d + 1] are staged once in
+// LDS (snake applied while staging) and every tap of the group reads its shifted view of the
+// window: 4 waves of 32 x 32 on v_mfma_f32_32x32x2_f32, KG accumulators each. Row strides are
+// odd (conflict-free reads).
+template <int KG>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
+  extern __shared__ float wsm[];
+  const int KT = 1 << a.kt_sh;
+  float* A_s = wsm;                    // [64][KT + 1]
+  float* X_s = wsm + 64 * (KT + 1);    // [64][WP]
   const int n_mt = (a.M + WG_BM - 1) / WG_BM, n_ct = (a.C + WG_BN - 1) / WG_BN;
   int bid = blockIdx.x;
   const int mt = bid % n_mt; bid /= n_mt;
   const int ct = bid % n_ct; bid /= n_ct;
-  const int k = bid % a.K;
-  const int sp = bid / a.K;
-  const int m0 = mt * WG_BM, c0 = ct * WG_BN;
+  const int kg = bid % a.n_kg;
+  const int sp = bid / a.n_kg;
+  const int m0 = mt * WG_BM, c0 = ct * WG_BN, k0 = kg * KG;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int nct = (a.TA + WG_KT - 1) / WG_KT;
+  const int nct = (a.TA + KT - 1) >> a.kt_sh;
   const int q0 = (int)((long long)sp * a.chunks / a.n_split);
   const int q1 = (int)((long long)(sp + 1) * a.chunks / a.n_split);
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  for (int q = q0; q < q1; ++q) {
-    const int b = q / nct, t0 = (q - b * nct) * WG_KT;
-    // stage A[b][m0..+64][t0..+32] and Xs[b][c0..+64][(t0..+32)*s - p + k*d]
-    for (int e = tid; e < WG_BM * WG_KT; e += 256) {
-      const int r = e / WG_KT, j = e - r * WG_KT;
-      const int m = m0 + r, t = t0 + j;
-      float av = 0.0f;
-      if (m < a.M && t < a.TA) {
-        av = a.A[((size_t)b * a.M + m) * a.TA + t];
-        if (a.alpha_a) av = snake_act(av, a.alpha_a[m], a.inv_alpha_a[m]);
+  // staging: wave w fills A rows and X-window rows w, w+4, ...; lanes walk the row (no index
+  // division, coalesced), snake applied on the fly. Loaded straight into LDS each chunk: the
+  // latency is covered by the other workgroups on the CU (small register / LDS footprint).
+  auto stage = [&](int q) {
+    const int b = q / nct, t0 = (q - b * nct) << a.kt_sh;
+    for (int r = wave; r < 64; r += 4) {
+      const int m = m0 + r;
+      const bool mok = m < a.M;
+      const float al = (mok && a.alpha_a) ? a.alpha_a[m] : 0.0f;
+      const float ial = (mok && a.alpha_a) ? a.inv_alpha_a[m] : 0.0f;
+      const float* ar = a.A + ((size_t)b * a.M + (mok ? m : 0)) * a.TA;
+      for (int j = lane; j < KT; j += 64) {
+        const int t = t0 + j;
+        float v = (mok && t < a.TA) ? ar[t] : 0.0f;
+        if (a.alpha_a) v = snake_act(v, al, ial);
+        A_s[r * (KT + 1) + j] = v;
       }
-      A_s[r][j] = av;
       const int c = c0 + r;
-      const int tx = t * a.s - a.p + k * a.d;
-      float v = 0.0f;
-      if (c < a.C && t < a.TA && tx >= 0 && tx < a.TX) {
-        v = a.X[((size_t)b * a.C + c) * a.TX + tx];
-        if (a.alpha) v = snake_act(v, a.alpha[c], a.inv_alpha[c]);
+      const bool cok = c < a.C;
+      const float cl = (cok && a.alpha) ? a.alpha[c] : 0.0f;
+      const float icl = (cok && a.alpha) ? a.inv_alpha[c] : 0.0f;
+      const float* xr = a.X + ((size_t)b * a.C + (cok ? c : 0)) * a.TX;
+      const int xb = t0 * a.s - a.p + k0 * a.d;
+      for (int pp = lane; pp < a.W; pp += 64) {
+        const int tx = xb + pp;
+        float v = (cok && tx >= 0 && tx < a.TX) ? xr[tx] : 0.0f;
+        if (a.alpha) v = snake_act(v, cl, icl);  // snake(0) = 0
+        X_s[r * a.WP + pp] = v;
       }
-      X_s[r][j] = v;
     }
+  };
+  f32x16 acc[KG];
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[kk][r] = 0.0f;
+  const float* arow = A_s + (wm * 32 + (lane & 31)) * (KT + 1) + (lane >> 5);
+  const float* xrow = X_s + (wn * 32 + (lane & 31)) * a.WP + (lane >> 5) * a.s;
+  for (int q = q0; q < q1; ++q) {
+    stage(q);
     __syncthreads();
     // 32x32x2: A lane l -> A[m = l & 31][kr = l >> 5]; B lane l -> B[kr = l >> 5][n = l & 31]
+    for (int tp = 0; tp < KT; tp += 2) {
+      const float av = arow[tp];
+      const float* xr = xrow + tp * a.s;
 #pragma unroll
-    for (int kk = 0; kk < WG_KT; kk += 2) {
-      const float av = A_s[wm * 32 + (lane & 31)][kk + (lane >> 5)];
-      const float bv = X_s[wn * 32 + (lane & 31)][kk + (lane >> 5)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      for (int kk = 0; kk < KG; ++kk)
+        acc[kk] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, xr[kk * a.d], acc[kk], 0, 0, 0);
     }
     __syncthreads();
   }
   // D: lane l, reg r -> row (r & 3) + 8 (r >> 2) + 4 (l >> 5), col l & 31
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    const int c = c0 + wn * 32 + (lane & 31);
-    if (m < a.M && c < a.C)
-      a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k] = acc[r];
-  }
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int c = c0 + wn * 32 + (lane & 31);
+      if (m < a.M && c < a.C && k0 + kk < a.K)
+        a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k0 + kk] = acc[kk][r];
+    }
 }
 
 // out[e] = sum_{s < n} part[s][e], split order
@@ -109,24 +138,27 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, size_t n_ele
 //   y = x + inv * sin(a x)^2,  inv = 1 / (a + 1e-9)
 //   dx = g * (1 + inv * (2 sin(a x) cos(a x)) * a)
 //   da = sum_{b,t} g * (-inv^2 * sin(a x)^2 + inv * (2 sin(a x) cos(a x)) * x)
-// One workgroup per (channel, split of the batch*time range); dalpha partials [split][C].
+// Workgroup = (channel c, split q = (clip b, time chunk of RCH)): coalesced row segments, no
+// per-element index division; dalpha partials [n_split][C] reduced in split order.
+constexpr int RCH = 4096;  // time samples per split
+
 __global__ __launch_bounds__(256) void snake_backward_kernel(
     const float* __restrict__ x, const float* __restrict__ alpha,
     const float* __restrict__ inv_alpha, const float* __restrict__ g, int B, int C, int T,
     int n_split, float* __restrict__ dx, float* __restrict__ da_part) {
   __shared__ float red[256];
-  const int c = blockIdx.x % C, sp = blockIdx.x / C;
+  const int c = blockIdx.x % C, q = blockIdx.x / C;
+  const int ntc = (T + RCH - 1) / RCH;
+  const int b = q / ntc, t0 = (q - b * ntc) * RCH, t1 = min(T, t0 + RCH);
   const float a = alpha[c], inv = inv_alpha[c];
-  const long long n = (long long)B * T;
-  const long long e0 = n * sp / n_split, e1 = n * (sp + 1) / n_split;
+  const size_t row = ((size_t)b * C + c) * T;
   float acc = 0.0f;
-  for (long long e = e0 + threadIdx.x; e < e1; e += 256) {
-    const int b = (int)(e / T), t = (int)(e - (long long)b * T);
-    const size_t o = ((size_t)b * C + c) * T + t;
-    const float xv = x[o], gv = g[o];
-    const float sn = sinf(a * xv), cs = cosf(a * xv);
+  for (int t = t0 + threadIdx.x; t < t1; t += 256) {
+    const float xv = x[row + t], gv = g[row + t];
+    float sn, cs;
+    sincos_reduced(a * xv, &sn, &cs);
     const float s2 = (2.0f * sn) * cs;
-    if (dx) dx[o] = gv * (1.0f + (inv * s2) * a);
+    if (dx) dx[row + t] = gv * (1.0f + (inv * s2) * a);
     acc += gv * (-(inv * inv) * (sn * sn) + (inv * s2) * xv);
   }
   red[threadIdx.x] = acc;
@@ -135,26 +167,26 @@ __global__ __launch_bounds__(256) void snake_backward_kernel(
     if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
     __syncthreads();
   }
-  if (threadIdx.x == 0 && da_part) da_part[(size_t)sp * C + c] = red[0];
+  if (threadIdx.x == 0 && da_part) da_part[(size_t)q * C + c] = red[0];
 }
 
-// db[c] (+)= sum_{b,t} g[b][c][t]; one workgroup per channel (fixed order)
+// db partials: workgroup (channel, split) as above, sum of g over the chunk
 __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ g, int B, int C,
-                                                        int T, float* __restrict__ db) {
+                                                        int T, float* __restrict__ part) {
   __shared__ float red[256];
-  const int c = blockIdx.x;
+  const int c = blockIdx.x % C, q = blockIdx.x / C;
+  const int ntc = (T + RCH - 1) / RCH;
+  const int b = q / ntc, t0 = (q - b * ntc) * RCH, t1 = min(T, t0 + RCH);
+  const float* gr = g + ((size_t)b * C + c) * T;
   float acc = 0.0f;
-  for (long long e = threadIdx.x; e < (long long)B * T; e += 256) {
-    const int b = (int)(e / T), t = (int)(e - (long long)b * T);
-    acc += g[((size_t)b * C + c) * T + t];
-  }
+  for (int t = t0 + threadIdx.x; t < t1; t += 256) acc += gr[t];
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int h = 128; h >= 1; h >>= 1) {
     if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
     __syncthreads();
   }
-  if (threadIdx.x == 0) db[c] = red[0];
+  if (threadIdx.x == 0) part[(size_t)q * C + c] = red[0];
 }
 
 // tanh / sigmoid backward from the stored output y (models/dac_vrvq.py:74,
@@ -222,11 +254,19 @@ unsigned grid_n(size_t total, unsigned block) {
 
 }  // namespace
 
+static int wgrad_kg(int k) {  // taps per workgroup: all of them up to 8 (k = 16: two groups)
+  if (k == 1 || k == 2 || k == 3 || k == 4 || k == 7 || k == 8) return k;
+  if (k % 8 == 0) return 8;
+  if (k % 4 == 0) return 4;
+  return 1;
+}
+
 extern "C" int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_split,
                                long long* workspace_bytes) {
   VRVQ_CHECK_ARG(n_split && workspace_bytes && batch > 0 && m > 0 && ta > 0 && c > 0 && k > 0);
-  const long long tiles = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) * k;
-  const long long chunks = (long long)batch * ((ta + WG_KT - 1) / WG_KT);
+  const long long tiles = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) *
+                          (k / wgrad_kg(k));
+  const long long chunks = (long long)batch * ((ta + 15) / 16);  // upper bound (KT >= 16)
   long long s = (1024 + tiles - 1) / tiles;  // >= 4 workgroups per CU in total
   if (s > chunks) s = chunks;
   if (s > 256) s = 256;
@@ -234,6 +274,16 @@ extern "C" int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_sp
   *n_split = (int)s;
   *workspace_bytes = s * m * (long long)c * k * (long long)sizeof(float);
   return 0;
+}
+
+template <int KG>
+int launch_wgrad(WgradArgs w, hipStream_t st) {
+  const long long nblk = (long long)((w.M + WG_BM - 1) / WG_BM) * ((w.C + WG_BN - 1) / WG_BN) *
+                         w.n_kg * w.n_split;
+  if (nblk >= 0x7fffffffLL) return VRVQ_ERR_ARG;
+  const size_t lds = (size_t)(64 * ((1 << w.kt_sh) + 1) + 64 * w.WP) * sizeof(float);
+  hipLaunchKernelGGL(wgrad_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
+  return vrvq_launch_status();
 }
 
 extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
@@ -246,31 +296,43 @@ extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
   VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
   VRVQ_CHECK_ARG(alpha_a == nullptr || inv_alpha_a != nullptr);
   VRVQ_CHECK_ARG(workspace_bytes >= (long long)n_split * m * (long long)c * k * 4);
+  const int kg = wgrad_kg(k);
   WgradArgs w{a, m, ta, x, c, tx, alpha_a, inv_alpha_a, alpha, inv_alpha, batch, k, stride, pad,
-              dil, n_split, 0, workspace};
-  w.chunks = batch * ((ta + WG_KT - 1) / WG_KT);
+              dil, n_split, 0, 5, 0, 0, k / kg, workspace};
+  // time chunk: 32 samples unless the window then exceeds the staging registers
+  for (w.kt_sh = 5; w.kt_sh >= 3; --w.kt_sh) {
+    w.W = ((1 << w.kt_sh) - 1) * stride + (kg - 1) * dil + 1;
+    if (w.W <= WG_WMAX) break;
+  }
+  if (w.W > WG_WMAX) return VRVQ_ERR_UNSUPPORTED;
+  w.WP = w.W | 1;
+  w.chunks = batch * ((ta + (1 << w.kt_sh) - 1) >> w.kt_sh);
   if (w.n_split > w.chunks) w.n_split = w.chunks;
-  const long long nblk = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) * k *
-                         w.n_split;
-  VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)nblk), dim3(256), 0, st, w);
+  int rc;
+  switch (kg) {
+    case 1: rc = launch_wgrad<1>(w, st); break;
+    case 2: rc = launch_wgrad<2>(w, st); break;
+    case 3: rc = launch_wgrad<3>(w, st); break;
+    case 4: rc = launch_wgrad<4>(w, st); break;
+    case 7: rc = launch_wgrad<7>(w, st); break;
+    default: rc = launch_wgrad<8>(w, st); break;
+  }
+  if (rc) return rc;
   const size_t n_elem = (size_t)m * c * k;
   hipLaunchKernelGGL(split_reduce_kernel, dim3(grid_n(n_elem, 256)), dim3(256), 0, st, workspace,
                      n_elem, w.n_split, out);
   return vrvq_launch_status();
 }
 
-static int snake_split(int batch, int frames) {
-  const long long n = (long long)batch * frames;
-  long long s = (n + 65535) / 65536;
-  return (int)(s > 64 ? 64 : (s < 1 ? 1 : s));
+static long long chunk_splits(int batch, int frames) {  // (clip, RCH-sample chunk) splits
+  return (long long)batch * ((frames + RCH - 1) / RCH);
 }
 
 extern "C" int vrvq_snake_backward_workspace(int batch, int channels, int frames,
                                              long long* bytes) {
   VRVQ_CHECK_ARG(bytes && batch > 0 && channels > 0 && frames > 0);
-  *bytes = (long long)snake_split(batch, frames) * channels * (long long)sizeof(float);
+  *bytes = chunk_splits(batch, frames) * channels * (long long)sizeof(float);
   return 0;
 }
 
@@ -280,23 +342,36 @@ extern "C" int vrvq_snake_backward(const float* x, const float* alpha, const flo
                                    long long workspace_bytes, vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(x && alpha && inv_alpha && grad && (dx || dalpha) && batch > 0 &&
                  channels > 0 && frames > 0);
-  const int n_split = snake_split(batch, frames);
-  if (dalpha) VRVQ_CHECK_ARG(workspace && workspace_bytes >= (long long)n_split * channels * 4);
+  const long long n_split = chunk_splits(batch, frames);
+  VRVQ_CHECK_ARG(n_split * channels < 0x7fffffffLL);
+  if (dalpha) VRVQ_CHECK_ARG(workspace && workspace_bytes >= n_split * channels * 4);
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(snake_backward_kernel, dim3((unsigned)(channels * n_split)), dim3(256), 0, st,
-                     x, alpha, inv_alpha, grad, batch, channels, frames, n_split, dx,
+                     x, alpha, inv_alpha, grad, batch, channels, frames, (int)n_split, dx,
                      dalpha ? workspace : nullptr);
   if (dalpha)
     hipLaunchKernelGGL(split_reduce_kernel, dim3(grid_n(channels, 256)), dim3(256), 0, st,
-                       workspace, (size_t)channels, n_split, dalpha);
+                       workspace, (size_t)channels, (int)n_split, dalpha);
   return vrvq_launch_status();
 }
 
+extern "C" int vrvq_bias_grad_workspace(int batch, int channels, int frames, long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && channels > 0 && frames > 0);
+  *bytes = chunk_splits(batch, frames) * channels * (long long)sizeof(float);
+  return 0;
+}
+
 extern "C" int vrvq_bias_grad(const float* grad, int batch, int channels, int frames, float* db,
-                              vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(grad && db && batch > 0 && channels > 0 && frames > 0);
-  hipLaunchKernelGGL(bias_grad_kernel, dim3(channels), dim3(256), 0, as_stream(stream), grad, batch,
-                     channels, frames, db);
+                              float* workspace, long long workspace_bytes, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(grad && db && workspace && batch > 0 && channels > 0 && frames > 0);
+  const long long n_split = chunk_splits(batch, frames);
+  VRVQ_CHECK_ARG(n_split * channels < 0x7fffffffLL);
+  VRVQ_CHECK_ARG(workspace_bytes >= n_split * channels * 4);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(bias_grad_kernel, dim3((unsigned)(channels * n_split)), dim3(256), 0, st,
+                     grad, batch, channels, frames, workspace);
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid_n(channels, 256)), dim3(256), 0, st,
+                     workspace, (size_t)channels, (int)n_split, db);
   return vrvq_launch_status();
 }
 
