@@ -59,34 +59,57 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
   const int nct = (a.TA + KT - 1) >> a.kt_sh;
   const int q0 = (int)((long long)sp * a.chunks / a.n_split);
   const int q1 = (int)((long long)(sp + 1) * a.chunks / a.n_split);
-  // staging: wave w fills A rows and X-window rows w, w+4, ...; lanes walk the row (no index
-  // division, coalesced), snake applied on the fly. Loaded straight into LDS each chunk: the
-  // latency is covered by the other workgroups on the CU (small register / LDS footprint).
+  // staging: wave w fills A rows and X-window rows w, w+4, ... (16 each), in two halves of 8
+  // rows: every load of a half is issued before its first LDS store (no per-row load -> store
+  // round trips; the half bounds the registers), lanes walk the rows (coalesced), snake applied
+  // between the loads and the stores.
+  constexpr int NA = 8 * 32 / 64;       // A values per lane per half (KT <= 32)
+  constexpr int NU = WG_WMAX / 64;      // X-window segments of 64 per row
   auto stage = [&](int q) {
     const int b = q / nct, t0 = (q - b * nct) << a.kt_sh;
-    for (int r = wave; r < 64; r += 4) {
-      const int m = m0 + r;
-      const bool mok = m < a.M;
-      const float al = (mok && a.alpha_a) ? a.alpha_a[m] : 0.0f;
-      const float ial = (mok && a.alpha_a) ? a.inv_alpha_a[m] : 0.0f;
-      const float* ar = a.A + ((size_t)b * a.M + (mok ? m : 0)) * a.TA;
-      for (int j = lane; j < KT; j += 64) {
-        const int t = t0 + j;
-        float v = (mok && t < a.TA) ? ar[t] : 0.0f;
-        if (a.alpha_a) v = snake_act(v, al, ial);
-        A_s[r * (KT + 1) + j] = v;
+    const int xb = t0 * a.s - a.p + k0 * a.d;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float av[NA], xv[8][NU];
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = lane + 64 * i;
+        const int r = wave + 4 * (8 * h + (e >> a.kt_sh)), j = e & (KT - 1);
+        const int m = m0 + r, t = t0 + j;
+        av[i] = (e < 8 * KT && m < a.M && t < a.TA) ? a.A[((size_t)b * a.M + m) * a.TA + t]
+                                                    : 0.0f;
       }
-      const int c = c0 + r;
-      const bool cok = c < a.C;
-      const float cl = (cok && a.alpha) ? a.alpha[c] : 0.0f;
-      const float icl = (cok && a.alpha) ? a.inv_alpha[c] : 0.0f;
-      const float* xr = a.X + ((size_t)b * a.C + (cok ? c : 0)) * a.TX;
-      const int xb = t0 * a.s - a.p + k0 * a.d;
-      for (int pp = lane; pp < a.W; pp += 64) {
-        const int tx = xb + pp;
-        float v = (cok && tx >= 0 && tx < a.TX) ? xr[tx] : 0.0f;
-        if (a.alpha) v = snake_act(v, cl, icl);  // snake(0) = 0
-        X_s[r * a.WP + pp] = v;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int c = c0 + wave + 4 * (8 * h + rr);
+        const float* xr = a.X + ((size_t)b * a.C + (c < a.C ? c : 0)) * a.TX;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int pp = lane + 64 * u, tx = xb + pp;
+          xv[rr][u] = (pp < a.W && c < a.C && tx >= 0 && tx < a.TX) ? xr[tx] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = lane + 64 * i;
+        if (e < 8 * KT) {
+          const int r = wave + 4 * (8 * h + (e >> a.kt_sh)), j = e & (KT - 1);
+          float v = av[i];
+          if (a.alpha_a && m0 + r < a.M)
+            v = snake_act(v, a.alpha_a[m0 + r], a.inv_alpha_a[m0 + r]);
+          A_s[r * (KT + 1) + j] = v;
+        }
+      }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = wave + 4 * (8 * h + rr), c = c0 + r;
+        const bool sn = a.alpha && c < a.C;
+        const float cl = sn ? a.alpha[c] : 0.0f, icl = sn ? a.inv_alpha[c] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int pp = lane + 64 * u;
+          if (pp < a.W) X_s[r * a.WP + pp] = sn ? snake_act(xv[rr][u], cl, icl) : xv[rr][u];
+        }
       }
     }
   };
