@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
   // rows: every load of a half is issued before its first LDS store (no per-row load -> store
   // round trips; the half bounds the registers), lanes walk the rows (coalesced), snake applied
   // between the loads and the stores.
-  constexpr int NA = 8 * 32 / 64;       // A values per lane per half (KT <= 32)
+  constexpr int NA = 8 * 64 / 64;       // A values per lane per half (KT <= 64)
   constexpr int NU = WG_WMAX / 64;      // X-window segments of 64 per row
   auto stage = [&](int q) {
     const int b = q / nct, t0 = (q - b * nct) << a.kt_sh;
@@ -289,7 +289,7 @@ extern "C" int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_sp
   VRVQ_CHECK_ARG(n_split && workspace_bytes && batch > 0 && m > 0 && ta > 0 && c > 0 && k > 0);
   const long long tiles = (long long)((m + WG_BM - 1) / WG_BM) * ((c + WG_BN - 1) / WG_BN) *
                           (k / wgrad_kg(k));
-  const long long chunks = (long long)batch * ((ta + 15) / 16);  // upper bound (KT >= 16)
+  const long long chunks = (long long)batch * ((ta + 7) / 8);  // upper bound (KT >= 8)
   long long s = (1024 + tiles - 1) / tiles;  // >= 4 workgroups per CU in total
   if (s > chunks) s = chunks;
   if (s > 256) s = 256;
@@ -322,8 +322,8 @@ extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
   const int kg = wgrad_kg(k);
   WgradArgs w{a, m, ta, x, c, tx, alpha_a, inv_alpha_a, alpha, inv_alpha, batch, k, stride, pad,
               dil, n_split, 0, 5, 0, 0, k / kg, workspace};
-  // time chunk: 32 samples unless the window then exceeds the staging registers
-  for (w.kt_sh = 5; w.kt_sh >= 3; --w.kt_sh) {
+  // time chunk: 64 samples unless the window then exceeds the staged row length
+  for (w.kt_sh = 6; w.kt_sh >= 3; --w.kt_sh) {
     w.W = ((1 << w.kt_sh) - 1) * stride + (kg - 1) * dil + 1;
     if (w.W <= WG_WMAX) break;
   }
