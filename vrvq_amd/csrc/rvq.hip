@@ -11,8 +11,9 @@
 // streams. Three launches:
 //
 //   rvq_project_kernel   P partials over 8 channel splits (v_mfma_f32_16x16x4_f32): each
-//                        workgroup streams one clip's 128-channel slab of z once (contiguous
-//                        rows, K chunks double-buffered in LDS under the MFMAs).
+//                        workgroup streams a 48-frame tile of one clip's 128-channel slab of
+//                        z once (all loads issued up front, 4 K chunks in their own LDS
+//                        buffers consumed as they land; two workgroups per CU).
 //   rvq_chain_kernel     the chain: <= 16 frames per workgroup, 8 waves; wave w scans its
 //                        N/8 codes for all frames at once on the matrix cores (16-code x
 //                        16-frame MFMA tiles), then 8 (frame, k) lane groups finish the stage
@@ -33,8 +34,8 @@ constexpr int RD = 1024;        // latent channels
 constexpr int RCD = 8;          // codebook_dim
 constexpr int PJ_SPLIT = 8;     // channel splits of the projection GEMM
 constexpr int PJ_CPS = RD / PJ_SPLIT;
-constexpr int PJ_TC = 96;       // frames per projection tile (6 MFMA column tiles)
-constexpr int PJ_ZLD = 112;     // z_s row stride (== 16 mod 32: conflict-free B reads)
+constexpr int PJ_TC = 48;       // frames per projection tile (3 MFMA column tiles)
+constexpr int PJ_ZLD = 48;      // z_s row stride (== 16 mod 32: conflict-free B reads)
 constexpr int PJ_WLD = 80;      // w_s row stride (== 16 mod 32: conflict-free A reads)
 constexpr int CH_NT = 512;      // chain threads (8 waves)
 constexpr int CH_NW = CH_NT / 64;
@@ -105,18 +106,19 @@ __global__ void rvq_frag_kernel(const float* __restrict__ cbn, int nq, int N,
 
 // ------------------------------------------------------------------------------------------
 // Projection: part[s][n][r] = sum_{c in split s} W_in_t[r/8][c][r%8] z[b][c][t], n = b*T + t,
-// r < R = nq*8. Workgroup = (clip b, frame tile of <= 96, channel split s, 64-row block), 8
-// waves: wave w computes rows 16 (w & 3) .. +15 for column tiles 3 (w >> 2) .. +2 with
-// v_mfma_f32_16x16x4_f32. All of the workgroup's loads (the [128 ch][96 t] slab of z: row
-// segments of one clip, and its [128][64] weight block) are issued up front, in 4 K chunks of
-// 32 channels, each chunk to its own LDS buffer: chunk c is stored (waiting only for its own
-// loads — they complete in issue order) and consumed by the MFMAs while chunks c+1.. are still
-// landing. One HBM round trip per workgroup instead of one per chunk. Output: lane l holds 4
+// r < R = nq*8. Workgroup = (clip b, frame tile of <= 48, channel split s, 64-row block), 4
+// waves: wave w computes rows 16 w .. +15 for the 3 column tiles with v_mfma_f32_16x16x4_f32.
+// All of the workgroup's loads (the [128 ch][48 t] slab of z: row segments of one clip, and its
+// [128][64] weight block) are issued up front, in 4 K chunks of 32 channels, each chunk to its
+// own LDS buffer: chunk c is stored (waiting only for its own loads -- they complete in issue
+// order) and consumed by the MFMAs while chunks c+1.. are still landing. 64 KB of LDS: two
+// workgroups per CU, so one's loads overlap the other's MFMAs. Output: lane l holds 4
 // consecutive rows of one frame -> one float4 store.
-constexpr int PJ_NT = 512;
+constexpr int PJ_NT = 256;
 constexpr int PJ_KC = 32;                       // channels per K chunk
 constexpr int PJ_NC = PJ_CPS / PJ_KC;           // chunks (4)
 constexpr int PJ_ZQ = PJ_KC * PJ_TC / PJ_NT;    // z loads per thread per chunk (6)
+constexpr int PJ_WQ = PJ_KC * 64 / 4 / PJ_NT;   // weight float4 per thread per chunk (2)
 constexpr int PJ_STG = PJ_KC * PJ_ZLD + PJ_KC * PJ_WLD;
 
 __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restrict__ z, int T,
@@ -133,22 +135,26 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
   float zv[PJ_NC][PJ_ZQ];
-  float4 wv[PJ_NC];
-  const int sl = tid >> 6, rem = tid & 63;
-  const int st = rb * 8 + sl;
+  float4 wv[PJ_NC][PJ_WQ];
 #pragma unroll
   for (int kc = 0; kc < PJ_NC; ++kc) {  // every load of the workgroup in flight at once
 #pragma unroll
     for (int q = 0; q < PJ_ZQ; ++q) {
       const int e = tid + PJ_NT * q;
       const int c = e / PJ_TC, t = e - c * PJ_TC;
-      zv[kc][q] = t < ntl ? zb[(size_t)(kc * PJ_KC + c) * T + t] : 0.0f;
+      // clamped address, zeroed at the LDS store (no branch: a guarded load becomes an
+      // exec-masked branch and the waitcnt pass then drains every outstanding load at the join)
+      zv[kc][q] = zb[(size_t)(kc * PJ_KC + c) * T + min(t, ntl - 1)];
     }
-    // 8 stages x 32 channels x 2 float4 = one float4 per thread
-    wv[kc] = st < nq ? ld4(w_in_t + ((size_t)st * RD + s * PJ_CPS + kc * PJ_KC) * RCD + rem * 4)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    // 8 stages x 32 channels x 2 float4
+#pragma unroll
+    for (int h = 0; h < PJ_WQ; ++h) {
+      const int e = tid + PJ_NT * h, sl = e >> 6, rem = e & 63;
+      const int st = rb * 8 + sl;
+      wv[kc][h] = ld4(w_in_t + ((size_t)min(st, nq - 1) * RD + s * PJ_CPS + kc * PJ_KC) * RCD +
+                      rem * 4);
+    }
   }
-  const int rt = wave & 3, cg = wave >> 2;
   const int lr = lane & 15, lk = lane >> 4;
   f32x4 acc[3];
 #pragma unroll
@@ -161,30 +167,39 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
     for (int q = 0; q < PJ_ZQ; ++q) {
       const int e = tid + PJ_NT * q;
       const int c = e / PJ_TC, t = e - c * PJ_TC;
-      z_s[c * PJ_ZLD + t] = zv[kc][q];
+      // bit mask, not a select: LLVM sinks a load whose only use is a select into a branch
+      z_s[c * PJ_ZLD + t] = __uint_as_float(__float_as_uint(zv[kc][q]) & (0u - (unsigned)(t < ntl)));
     }
-    *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) = wv[kc];
+#pragma unroll
+    for (int h = 0; h < PJ_WQ; ++h) {
+      const int e = tid + PJ_NT * h, sl = e >> 6, rem = e & 63;
+      const unsigned m = 0u - (unsigned)(rb * 8 + sl < nq);
+      const float4 w = wv[kc][h];
+      *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) =
+          make_float4(__uint_as_float(__float_as_uint(w.x) & m), __uint_as_float(__float_as_uint(w.y) & m),
+                      __uint_as_float(__float_as_uint(w.z) & m), __uint_as_float(__float_as_uint(w.w) & m));
+    }
     __syncthreads();
     // all column tiles unconditionally (zero-padded frames): a runtime-guarded MFMA makes the
     // compiler shuffle the accumulators through v_mov / accvgpr copies every step
 #pragma unroll
     for (int kk = 0; kk < PJ_KC / 4; ++kk) {
       const int c = kk * 4 + lk;
-      const float av = w_s[c * PJ_WLD + rt * 16 + lr];
+      const float av = w_s[c * PJ_WLD + wave * 16 + lr];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const float bv = z_s[c * PJ_ZLD + (cg * 3 + j) * 16 + lr];
+        const float bv = z_s[c * PJ_ZLD + j * 16 + lr];
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
       }
     }
   }
-  const int r0 = rb * 64 + rt * 16;
+  const int r0 = rb * 64 + wave * 16;
   // D layout: lane l, reg q -> row 4*(l>>4) + q of the wave's 16, column (frame) l & 15
   const int rr = r0 + 4 * lk;  // R = 8 nq: rows rr..rr+3 are all valid iff rr < R
   if (rr >= R) return;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int t = (cg * 3 + j) * 16 + lr;
+    const int t = j * 16 + lr;
     if (t < ntl) {
       const size_t n = (size_t)b * T + t0 + t;
       *reinterpret_cast<float4*>(part + ((size_t)s * NF + n) * R + rr) =
@@ -438,17 +453,24 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
       vrvq::amin(best, bidx, vrvq::xchg<16>(best, lane), vrvq::xchg<16>(bidx, lane));
       vrvq::amin(best, bidx, vrvq::xchg<32>(best, lane), vrvq::xchg<32>(bidx, lane));
       // the candidate's raw codebook row (L2 gather, models/quantize.py:101-103): only the
-      // wave's own candidates, so no per-stage staging of the whole raw codebook. Issued
-      // before the next stage's prefetch, so the wait for it does not cover the prefetch.
+      // wave's own candidates, so no per-stage staging of the whole raw codebook (measured: an
+      // LDS copy of the stage's codebook, prefetched a stage ahead, is slower -- the gather's
+      // latency hides behind the other wave of the SIMD). Issued before the next stage's
+      // prefetch, so the wait for it does not cover the prefetch.
       const float* row = a.cb + ((size_t)i * N + (lane < nf ? bidx : 0)) * RCD;
       const float4 r0 = ld4(row), r1 = ld4(row + 4);
-      if (more) {  // stage i+1 operands (cbn fragments, c2 slice, M column)
-        load_a(i + 1, an);
+      __builtin_amdgcn_sched_barrier(0);  // keep the gather ahead of the prefetch (vmcnt order)
+      {  // stage i+1 operands (cbn fragments, c2 slice, M column). Unconditional loads from
+         // clamped addresses (the last stage re-reads its own): a branch around them makes the
+         // waitcnt pass assume none are outstanding at the join, so the candidate-row wait
+         // below would drain the whole prefetch.
+        const int in = more ? i + 1 : i;
+        load_a(in, an);
 #pragma unroll
         for (int q = 0; q < C2W; ++q)
-          c2n[q] = lane + 64 * q < NPW ? a.c2[(size_t)(i + 1) * N + cw + lane + 64 * q] : 0.0f;
-        if (i + 2 < nq && tid * 4 < R * RCD)  // M_{.,i+1}: needed from stage i+1 on
-          mn = ld4(a.mcol + (size_t)(i + 1) * R * RCD + tid * 4);
+          c2n[q] = a.c2[(size_t)in * N + cw + min(lane + 64 * q, NPW - 1)];
+        // M_{.,i+1}: needed from stage i+1 on (stored only when i + 2 < nq)
+        mn = ld4(a.mcol + (size_t)min(i + 1, nq - 1) * R * RCD + min(tid * 4, R * RCD - 4));
       }
       deferred_updates();
       if (lane < nf) {
