@@ -73,12 +73,23 @@ def _fake():
                 torch.empty(B, nq, T), torch.empty(B, nq, D, T), torch.empty(B, D, T),
                 torch.empty(B, nq, T))
 
+    def rvq_encode(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None, level=1.0,
+                   want_z_q_is=True, want_mask=True):
+        B, D, T = z.shape
+        nq = cb.shape[0]
+        return (torch.zeros(B, nq, T, dtype=torch.long), torch.empty(B, nq * 8, T),
+                torch.empty(B, nq, T), torch.empty(B, nq, D, T) if want_z_q_is else None,
+                torch.empty(B, D, T), torch.empty(B, nq, T) if want_mask else None)
+
+    ops.rvq_encode = rvq_encode
+    ops.rvq_frag = lambda cbn: cbn
     ops.rvq_codes = rvq_codes
     ops.rvq_expand = rvq_expand
     ops.rvq_fused = rvq_fused
     ops.rvq_cross_prep = lambda wi, wo, bo: (torch.zeros(wi.shape[0], wi.shape[0], 8, 8),
                                              torch.zeros(wi.shape[0], 8))
     ops.masked_loss = lambda l, m: torch.zeros(())
+    ops.imp_mask = lambda *a, **k: None
 
 
 def main():

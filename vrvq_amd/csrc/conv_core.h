@@ -3,6 +3,7 @@
 // LDS-transposed epilogue. See conv.hip for the GEMM mapping and the MFMA operand layouts.
 #pragma once
 #include "common.h"
+#include <type_traits>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -361,22 +362,73 @@ __device__ __forceinline__ void conv_epilogue(
       }
     } else {
       // transposed conv: GEMM row m = co*up + phase, column n -> t = n*up + phase - up_pad.
-      // Walk (channel, t) so consecutive lanes store consecutive t.
-      const int up = a.up, tl_n = BNP * up;
-      const int co0 = m0 / up, nco = min(BM / up, a.cout - co0);
-      for (int e = tid; e < BM * BNP; e += NT) {
-        const int cl = e / tl_n, tl = e - cl * tl_n;
-        const int nl = tl / up, ph = tl - nl * up;
-        const int t = (p0 + nl) * up + ph - a.up_pad;
-        if (cl < nco && p0 + nl < a.ng && t >= 0 && t < a.ylen) {
-          const int co = co0 + cl;
-          float v = ct[(cl * up + ph) * BNP + nl];
-          if (a.bias) v = v + a.bias[co];
-          const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
-          if (a.y) a.y[o] = v;
-          if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[co], a.inv_alpha_o[co]);
+      // Walk (channel, t) so consecutive lanes store consecutive t. The decoder's strides
+      // (2, 4, 8) get compile-time index arithmetic (shifts instead of integer divisions).
+      auto walk = [&](auto up_c) {
+        constexpr int UPC = decltype(up_c)::value;
+        const int up = UPC ? UPC : a.up, tl_n = BNP * up;
+        const int co0 = m0 / up, nco = min(BM / up, a.cout - co0);
+        for (int e = tid; e < BM * BNP; e += NT) {
+          const int cl = e / tl_n, tl = e - cl * tl_n;
+          const int nl = tl / up, ph = tl - nl * up;
+          const int t = (p0 + nl) * up + ph - a.up_pad;
+          if (cl < nco && p0 + nl < a.ng && t >= 0 && t < a.ylen) {
+            const int co = co0 + cl;
+            float v = ct[(cl * up + ph) * BNP + nl];
+            if (a.bias) v = v + a.bias[co];
+            const size_t o = ((size_t)b * a.cout + co) * a.ylen + t;
+            if (a.y) a.y[o] = v;
+            if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[co], a.inv_alpha_o[co]);
+          }
         }
-      }
+      };
+      // Strides 2 / 4 / 8: each thread owns 4 consecutive output samples of one channel and
+      // stores them as one 16-B vector (dword-aligned: t0 = p0*up + 4q - up_pad).
+      auto walk4 = [&](auto up_c) {
+        constexpr int UP = decltype(up_c)::value;
+        constexpr int QN = BNP * UP / 4;  // quads per channel row of the tile
+        const int co0 = m0 / UP, nco = min(BM / UP, a.cout - co0);
+        for (int q = tid; q < (BM / UP) * QN; q += NT) {
+          const int cl = q / QN, tl0 = (q - cl * QN) * 4;
+          const int t0 = p0 * UP + tl0 - a.up_pad;
+          if (cl >= nco) continue;
+          const int co = co0 + cl;
+          const float bb = a.bias ? a.bias[co] : 0.0f;
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int tl = tl0 + u, nl = tl / UP, ph = tl - nl * UP;
+            v[u] = ct[(cl * UP + ph) * BNP + nl];
+            if (a.bias) v[u] = v[u] + bb;
+          }
+          const size_t o = ((size_t)b * a.cout + co) * a.ylen + t0;
+          const bool full = p0 + (tl0 + 3) / UP < a.ng && t0 >= 0 && t0 + 3 < a.ylen;
+          float sv[4];
+          if (a.ys) {
+            const float al = a.alpha_o[co], ia = a.inv_alpha_o[co];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sv[u] = snake_act(v[u], al, ia);
+          }
+          if (full) {
+            typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+            if (a.y) *reinterpret_cast<f4u*>(a.y + o) = f4u{v[0], v[1], v[2], v[3]};
+            if (a.ys) *reinterpret_cast<f4u*>(a.ys + o) = f4u{sv[0], sv[1], sv[2], sv[3]};
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int t = t0 + u;
+              if (p0 + (tl0 + u) / UP < a.ng && t >= 0 && t < a.ylen) {
+                if (a.y) a.y[o + u] = v[u];
+                if (a.ys) a.ys[o + u] = sv[u];
+              }
+            }
+          }
+        }
+      };
+      if (a.up == 8 && BM % 8 == 0) walk4(std::integral_constant<int, 8>{});
+      else if (a.up == 4 && BM % 4 == 0) walk4(std::integral_constant<int, 4>{});
+      else if (a.up == 2) walk4(std::integral_constant<int, 2>{});
+      else walk(std::integral_constant<int, 0>{});
     }
   }
 }
