@@ -29,6 +29,8 @@ def main():
                     help="fused ResidualUnit (k7 dil --dil, k1, skip) with cin channels")
     ap.add_argument("--snake-in", action="store_true", help="Snake on load (consumer side)")
     ap.add_argument("--no-snake-out", action="store_true", help="no producer-side Snake output")
+    ap.add_argument("--raw", action="store_true",
+                    help="also write the raw output next to the Snake one (encoder blocks)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
@@ -65,7 +67,7 @@ def main():
         tout = (args.t + 2 * pad - args.dil * (args.k - 1) - 1) // args.stride + 1
         res = torch.randn(args.batch, args.cout, tout, device=dev) if args.res else None
         fn = lambda: ops.conv1d(x, wp, args.cout, cp, args.k, args.stride, pad, args.dil, b, a_in,
-                                i_in, res, out_snake=osn, want_raw=args.res or osn is None)
+                                i_in, res, out_snake=osn, want_raw=args.raw or args.res or osn is None)
         flops = 2.0 * args.batch * args.cin * args.cout * args.k * tout
     for _ in range(3):
         fn()

@@ -136,7 +136,7 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   // transposed conv: a tile must hold whole output channels (rows co*up .. co*up + up-1), the
   // epilogue maps rows back with co0 = m0 / up
   if (a.up > 0 && BM % a.up != 0) return VRVQ_ERR_UNSUPPORTED;
-  constexpr int CK = ChunkCfg<KS, BM>::CK;
+  constexpr int CK = ChunkCfg<KS, BM, BN>::CK;
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
   const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
   const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;

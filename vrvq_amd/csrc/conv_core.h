@@ -33,11 +33,17 @@ struct ConvArgs {
   int n_mt, n_nt;          // M tiles, N tiles
 };
 
-template <int KS, int BM>
+template <int KS, int BM, int BN>
 struct ChunkCfg {
   // Input channels per K-chunk: CK*KS ~ 32..64 rows of W per stage (half for 192-row tiles,
   // so two double-buffered stages still fit twice per CU).
-  static constexpr int CK0 = KS == 1 ? 32 : KS <= 4 ? 16 : KS <= 8 ? 8 : 4;
+  // The strided encoder convs (KS = 2 s in {4, 8, 16}) take half of that: with their wide
+  // input windows a full chunk needs ~99 KB for the two stages, one workgroup per CU, and
+  // their short K then leaves every prologue / epilogue exposed (measured at B = 32:
+  // 64->128 s2 877 -> 680 us, 128->256 s4 1279 -> 1072, 512->1024 s8 at BN 32 888 -> 696;
+  // but 256->512 s8 at BN 128 1319 -> 1606, so k16 keeps 4 channels on 128-wide tiles).
+  static constexpr int CK0 = KS == 1 ? 32 : KS <= 3 ? 16 : KS == 4 ? 8 : KS == 7 ? 8
+                             : KS == 8 ? 4 : BN > 32 ? 4 : 2;
   static constexpr int CK = (BM > 128 && CK0 >= 8) ? CK0 / 2 : CK0;
 };
 
@@ -93,7 +99,7 @@ __device__ __forceinline__ void conv_mainloop(
   constexpr int TN = BN / WN;
   constexpr int RM = TM / 32;
   constexpr int RN = TN / 32;
-  constexpr int CK = ChunkCfg<KS, BM>::CK;
+  constexpr int CK = ChunkCfg<KS, BM, BN>::CK;
   constexpr int KROWS = CK * KS;
   constexpr int WQ4 = KROWS * BM / 4;               // float4 of W per chunk
   constexpr int WQ = (WQ4 + NT - 1) / NT;           // ... per thread

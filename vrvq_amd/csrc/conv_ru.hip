@@ -120,7 +120,7 @@ __global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
 
 template <int BM, int BN, int WM, int NW>
 int launch_ru(RuArgs ra, int batch, hipStream_t st) {
-  constexpr int CK = ChunkCfg<7, BM>::CK;
+  constexpr int CK = ChunkCfg<7, BM, BN>::CK;
   ConvArgs& a = ra.p1;
   a.n_mt = 1;
   a.n_nt = (a.ng + BN - 1) / BN;
