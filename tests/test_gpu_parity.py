@@ -141,6 +141,8 @@ CONV_CASES = [
     (2, 256, 512, 256, 16, 8, 4, 1, True, False, 0),
     (2, 1024, 1024, 87, 3, 1, 1, 1, True, False, 0),
     (2, 96, 1, 1000, 7, 1, 3, 1, True, False, 1),
+    (1, 96, 1, 2052, 7, 1, 3, 1, False, True, 1),    # Cout = 1 stream: tail tile + residual
+    (2, 5, 1, 36, 3, 1, 1, 1, True, False, 0),       # stream k3: channel remainder, edges
     (2, 8, 1, 87, 3, 1, 1, 1, True, False, 2),
     (2, 32, 8, 87, 3, 1, 1, 1, True, False, 0),
     (1, 1024, 1536, 87, 7, 1, 3, 1, False, False, 0),
@@ -195,6 +197,25 @@ def test_conv1d_vs_torch(case):
         else:
             assert y2 is None
         assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("k,p", [(7, 3), (3, 1)])
+def test_cout1_stream_matches_small_kernel(k, p):
+    """The Cout = 1 stream kernel (tin % 4 == 0) and the LDS-staged small-Cout kernel (other
+    lengths) share the (channel, tap) fmaf order: outputs away from the right edge agree bit
+    for bit between a length-1000 input and the same input extended to 1001."""
+    gen = torch.Generator(device="cpu").manual_seed(11 + k)
+    x = (torch.rand(2, 96, 1001, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(1, 96, k, generator=gen) / np.sqrt(96 * k)).to(DEV)
+    b = (torch.randn(1, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(96, generator=gen) * 1.5 + 0.5).to(DEV)
+    wp, cp = ops.pack_conv1d_weight(w)
+    ia = ops.snake_inv_alpha(alpha)
+    y0 = ops.conv1d(x[..., :1000].contiguous(), wp, 1, cp, k, 1, p, 1, bias=b, alpha=alpha,
+                    inv_alpha=ia, epilogue=ops.EPI_TANH)
+    y1 = ops.conv1d(x, wp, 1, cp, k, 1, p, 1, bias=b, alpha=alpha, inv_alpha=ia,
+                    epilogue=ops.EPI_TANH)
+    assert torch.equal(y0[..., :990], y1[..., :990])
 
 
 @pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8), (2, 384, 192, 333, 4),

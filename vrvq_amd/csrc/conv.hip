@@ -114,7 +114,110 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
   }
 }
 
+// Cout = 1 as a stream (the decoder's 96->1 k7 + Tanh, HBM-bound on reading x): no LDS, no
+// barriers; each thread owns 4 consecutive outputs and per input channel reads the 12-sample
+// window t0-4 .. t0+7 as three 16-B loads (covers pad <= 4 and k-1-pad <= 4 at dilation 1),
+// channels unrolled by 8 so their loads are in flight together (measured at B = 32, 96 -> 1 k7:
+// 364 us for the LDS-staged kernel, 277 us at 8 outputs x 4 channels per thread, 235 us at
+// 4 x 8, 163 us (3.4 TB/s) with the window / Snake branches hoisted out of the channel loop). Accumulation order per output:
+// channel, then tap -- conv_small_cout_kernel's fmaf chain, so the two agree bit for bit.
+constexpr int C1_T = 4;
+constexpr int C1_W = 12;  // window samples per channel
+template <int KS, int PAD>
+__global__ __launch_bounds__(256) void conv_cout1_stream_kernel(ConvArgs a) {
+  static_assert(PAD <= 4 && 4 - PAD + KS - 1 + C1_T - 1 < C1_W, "window t0-4 .. t0+7");
+  constexpr int SH = 4 - PAD;  // window index of tap 0 for output t0
+  const int n_t = (a.ng + 256 * C1_T - 1) / (256 * C1_T);
+  const int b = blockIdx.x / n_t;
+  const int t0 = ((blockIdx.x - b * n_t) * 256 + (int)threadIdx.x) * C1_T;
+  if (t0 >= a.ng) return;  // no barrier in this kernel
+  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  const bool interior = t0 - 4 >= 0 && t0 - 4 + C1_W <= a.tin;
+  float acc[C1_T];
+#pragma unroll
+  for (int u = 0; u < C1_T; ++u) acc[u] = 0.0f;
+  // the window path and the Snake flag are decided once, outside the channel loop: a branch
+  // per channel would drain each channel's loads before the next are issued
+  auto run = [&](auto interior_c, auto snake_c) {
+    constexpr bool INTERIOR = decltype(interior_c)::value, SNAKE = decltype(snake_c)::value;
+    auto load_win = [&](int c, float (&xv)[C1_W]) {
+      const float* xr = xb + (size_t)c * a.tin + t0 - 4;
+      if constexpr (INTERIOR) {
+#pragma unroll
+        for (int q = 0; q < C1_W / 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(xr + 4 * q);
+          xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < C1_W; ++j) {
+          const int t = t0 - 4 + j;
+          const float v = xb[(size_t)c * a.tin + min(max(t, 0), a.tin - 1)];
+          xv[j] = __uint_as_float(__float_as_uint(v) & (0u - (unsigned)(t >= 0 && t < a.tin)));
+        }
+      }
+    };
+    auto accum = [&](int c, float (&xv)[C1_W]) {
+      if constexpr (SNAKE) {
+        const float al = a.alpha[c], ia = a.inv_alpha[c];
+#pragma unroll
+        for (int j = 0; j < C1_W; ++j) xv[j] = snake_act(xv[j], al, ia);  // snake(0) = 0
+      }
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const float wv = a.w[(size_t)(c * KS + k) * a.m_pad];
+#pragma unroll
+        for (int u = 0; u < C1_T; ++u) acc[u] = fmaf(wv, xv[SH + k + u], acc[u]);
+      }
+    };
+    constexpr int CU = 8;
+    int c = 0;
+    for (; c + CU <= a.cin; c += CU) {
+      float xv[CU][C1_W];
+#pragma unroll
+      for (int i = 0; i < CU; ++i) load_win(c + i, xv[i]);
+#pragma unroll
+      for (int i = 0; i < CU; ++i) accum(c + i, xv[i]);
+    }
+    for (; c < a.cin; ++c) {
+      float xv[C1_W];
+      load_win(c, xv);
+      accum(c, xv);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (interior) {
+    if (a.alpha) run(T_{}, T_{}); else run(T_{}, F_{});
+  } else {
+    if (a.alpha) run(F_{}, T_{}); else run(F_{}, F_{});
+  }
+#pragma unroll
+  for (int u = 0; u < C1_T; ++u) {
+    const int t = t0 + u;
+    if (t < a.ng) {
+      float v = acc[u];
+      if (a.bias) v = v + a.bias[0];
+      const size_t o = (size_t)b * a.ylen + t;
+      if (a.res) v = a.res[o] + v;
+      v = apply_epi(v, a.epi);
+      if (a.y) a.y[o] = v;
+      if (a.ys) a.ys[o] = snake_act(v, a.alpha_o[0], a.inv_alpha_o[0]);
+    }
+  }
+}
+
 int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
+  if (a.M == 1 && a.cout == 1 && a.stride == 1 && a.dil == 1 && a.tin % 4 == 0 &&
+      ((ks == 7 && a.pad == 3) || (ks == 3 && a.pad == 1))) {
+    const long long nblk = (long long)batch * ((a.ng + 256 * C1_T - 1) / (256 * C1_T));
+    if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+    if (ks == 7)
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<7, 3>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<3, 1>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+    return vrvq_launch_status();
+  }
   if (a.cin * ks * (a.M == 1 ? 1 : SMALL_COUT) > SMALL_WMAX) return VRVQ_ERR_UNSUPPORTED;
   const size_t lds = (size_t)(SMALL_WMAX + SMALL_SC * (SMALL_BT + (ks - 1) * a.dil)) * sizeof(float);
   if (lds > 64 * 1024) return VRVQ_ERR_UNSUPPORTED;
