@@ -122,6 +122,15 @@ int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin, const flo
                           const float* alpha_out, const float* inv_alpha_out, float* y_snake,
                           vrvq_stream_t stream);
 
+/* vrvq_conv_transpose1d with an explicit padding 0 <= pad < stride: y has length
+ * (tin - 1)*stride - 2*pad + 2*stride. pad = 0 is the padding=False window of the chunked
+ * codec (CodecMixin.padding setter, models/dac_base.py:68-84: every conv's padding -> 0). */
+int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int tin, const float* alpha,
+                              const float* inv_alpha, const float* w_packed, int cout,
+                              int cout_pad, int stride, int pad, const float* bias, float* y,
+                              const float* alpha_out, const float* inv_alpha_out,
+                              float* y_snake, vrvq_stream_t stream);
+
 /* Pack a folded ConvTranspose1d weight w[Cin][Cout][2*stride] into the polyphase layout. */
 int vrvq_pack_convt1d_weight(const float* w, int cin, int cout, int stride, int cout_pad,
                              float* w_packed, vrvq_stream_t stream);

@@ -31,6 +31,9 @@ class TorchRef:
         self.n_codebooks = n_codebooks
         self.model_type = model_type
         self.hop = int(np.prod(encoder_rates))
+        # padding=False (models/dac_base.py:68-84, the chunked codec): encoder / decoder convs
+        # unpadded, residual skips centre-cropped (models/layers.py:65-67)
+        self.valid = False
         # weight norm folded once (the reference recomputes it in a pre-hook every forward:
         # the same expression, models/layers.py:17-22 -> torch._weight_norm over dims != 0)
         self.w = {}
@@ -49,35 +52,45 @@ class TorchRef:
 
     # models/layers.py:52-68
     def residual_unit(self, x, pre, dil):
-        y = self.conv(self.snake(x, pre + ".block.0"), pre + ".block.1", pad=3 * dil, dil=dil)
+        y = self.conv(self.snake(x, pre + ".block.0"), pre + ".block.1", pad=self._p(3 * dil),
+                      dil=dil)
         y = self.conv(self.snake(y, pre + ".block.2"), pre + ".block.3")
+        pad = (x.shape[-1] - y.shape[-1]) // 2
+        if pad > 0:
+            x = x[..., pad:-pad]
         return x + y
+
+    def _p(self, pad):
+        return 0 if self.valid else pad
 
     # models/dac_vrvq.py:39-48 with models/layers.py:71-89
     def encoder(self, x):
-        x = self.conv(x, "encoder.block.0", pad=3)
+        x = self.conv(x, "encoder.block.0", pad=self._p(3))
         for i, s in enumerate(self.encoder_rates):
             pre = f"encoder.block.{i + 1}"
             for j, d in enumerate((1, 3, 9)):
                 x = self.residual_unit(x, f"{pre}.block.{j}", d)
             x = self.conv(self.snake(x, pre + ".block.3"), pre + ".block.4", stride=s,
-                          pad=math.ceil(s / 2))
+                          pad=self._p(math.ceil(s / 2)))
         feat = x
         n = len(self.encoder_rates) + 1
-        return self.conv(self.snake(x, f"encoder.block.{n}"), f"encoder.block.{n + 1}", pad=1), feat
+        z = self.conv(self.snake(x, f"encoder.block.{n}"), f"encoder.block.{n + 1}", pad=self._p(1))
+        p = (feat.shape[-1] - z.shape[-1]) // 2  # padding=False: feat cropped to z's frames
+        return z, (feat[..., p:feat.shape[-1] - p] if p > 0 else feat)
 
     # models/dac_vrvq.py:79-80 with models/layers.py:92-110
     def decoder(self, z):
-        x = self.conv(z, "decoder.model.0", pad=3)
+        x = self.conv(z, "decoder.model.0", pad=self._p(3))
         for i, s in enumerate(self.decoder_rates):
             pre = f"decoder.model.{i + 1}"
             q = pre + ".block.1"
             x = F.conv_transpose1d(self.snake(x, pre + ".block.0"), self.w[q], self.p[q + ".bias"],
-                                   stride=s, padding=math.ceil(s / 2))
+                                   stride=s, padding=self._p(math.ceil(s / 2)))
             for j, d in zip((2, 3, 4), (1, 3, 9)):
                 x = self.residual_unit(x, f"{pre}.block.{j}", d)
         n = len(self.decoder_rates) + 1
-        x = self.conv(self.snake(x, f"decoder.model.{n}"), f"decoder.model.{n + 1}", pad=3)
+        x = self.conv(self.snake(x, f"decoder.model.{n}"), f"decoder.model.{n + 1}",
+                      pad=self._p(3))
         return torch.tanh(x)
 
     # models/importance_subnet.py:38-45

@@ -28,6 +28,8 @@ SIGNATURES = {
     "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P,
                            _P],
     "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "vrvq_conv_transpose1d_pad": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P,
+                                  _P],
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
     "vrvq_rvq_cross_prep": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "vrvq_rvq_frag": [_P, _I, _I, _I, _P, _P],

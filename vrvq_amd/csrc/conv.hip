@@ -459,12 +459,26 @@ extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin
                                      const float* bias, float* y, const float* alpha_out,
                                      const float* inv_alpha_out, float* y_snake,
                                      vrvq_stream_t stream) {
+  // math.ceil(stride / 2), models/layers.py:102
+  return vrvq_conv_transpose1d_pad(x, batch, cin, tin, alpha, inv_alpha, w_packed, cout,
+                                   cout_pad, stride, (stride + 1) / 2, bias, y, alpha_out,
+                                   inv_alpha_out, y_snake, stream);
+}
+
+extern "C" int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int tin,
+                                         const float* alpha, const float* inv_alpha,
+                                         const float* w_packed, int cout, int cout_pad,
+                                         int stride, int pad, const float* bias, float* y,
+                                         const float* alpha_out, const float* inv_alpha_out,
+                                         float* y_snake, vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
   VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && stride > 0);
+  // pad 0 = the padding=False windows of the chunked codec (models/dac_base.py:72-82)
+  VRVQ_CHECK_ARG(pad >= 0 && pad < stride);
   VRVQ_CHECK_ARG(cout_pad >= cout * stride && cout_pad % 64 == 0);
   VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
-  const int p = (stride + 1) / 2;  // math.ceil(stride / 2), models/layers.py:102
+  const int p = pad;
   ConvArgs a{};
   a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
   a.res = nullptr; a.y = y;

@@ -194,27 +194,30 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
     const Tensor& x, const Tensor& w_packed, int64_t cout, int64_t stride,
     const optional<Tensor>& bias, const optional<Tensor>& alpha,
     const optional<Tensor>& inv_alpha, const optional<Tensor>& alpha_out,
-    const optional<Tensor>& inv_alpha_out, bool want_raw) {
+    const optional<Tensor>& inv_alpha_out, bool want_raw, int64_t pad) {
   check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
   check_opt(alpha, x, "alpha");
   check_opt(inv_alpha, x, "inv_alpha");
   TORCH_CHECK(x.dim() == 3, "conv_transpose1d: x must be (B, C, T)");
+  // pad -1: the DecoderBlock's ceil(stride / 2); 0: padding=False (models/dac_base.py:68-84)
+  const int64_t p = pad < 0 ? (stride + 1) / 2 : pad;
+  TORCH_CHECK(p < stride, "conv_transpose1d: padding must be < stride");
   TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1) && w_packed.size(1) == 2,
               "conv_transpose1d: w_packed must be (Cin, 2, cout_pad)");
   TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(),
               "conv_transpose1d: snake needs inv_alpha");
   c10::DeviceGuard guard(x.device());
   const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
-  const int64_t p = (stride + 1) / 2;
   const int64_t tout = (tin - 1) * stride - 2 * p + 2 * stride;
   auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
-  check_rc(vrvq_conv_transpose1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                                 fp(inv_alpha), w_packed.data_ptr<float>(), (int)cout,
-                                 (int)w_packed.size(2), (int)stride, fp(bias), opt_ptr(y),
-                                 fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
-           "vrvq_conv_transpose1d");
+  check_rc(vrvq_conv_transpose1d_pad(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                                     fp(inv_alpha), w_packed.data_ptr<float>(), (int)cout,
+                                     (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
+                                     opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
+                                     stream_of(x)),
+           "vrvq_conv_transpose1d_pad");
   return {y, ys};
 }
 
@@ -827,7 +830,7 @@ TORCH_LIBRARY(vrvq, m) {
   m.def(
       "snake_conv_transpose1d(Tensor x, Tensor w_packed, int cout, int stride, Tensor? bias, "
       "Tensor? alpha, Tensor? inv_alpha, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw) -> (Tensor, Tensor)");
+      "bool want_raw, int pad=-1) -> (Tensor, Tensor)");
   m.def(
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "

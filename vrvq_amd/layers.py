@@ -144,7 +144,7 @@ class WNConvTranspose1d(nn.Module):
         return ops.conv_transpose1d(x, wp, self.out_channels, cout_pad, self.stride[0],
                                     bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                                     out_snake=None if out_snake is None else out_snake.prepared(),
-                                    want_raw=want_raw)
+                                    want_raw=want_raw, pad=self.padding[0])
 
 
 class ResidualUnit(nn.Module):
@@ -164,7 +164,11 @@ class ResidualUnit(nn.Module):
 
     def forward(self, x):
         y = self.block[1](x, snake=self.block[0])
-        # "same" padding: the reference's centre crop (:65-67) never triggers.
+        # centre crop of the skip (:65-67): only with padding=False (the chunked codec), where
+        # the k7 conv runs unpadded; with "same" padding it never triggers.
+        pad = (x.shape[-1] - y.shape[-1]) // 2
+        if pad > 0:
+            x = x[..., pad:-pad].contiguous()
         return self.block[3](y, snake=self.block[2], residual=x)
 
     def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool):

@@ -31,14 +31,29 @@ class Encoder(nn.Module):
             blocks += [EncoderBlock(d_model, stride=stride)]
         blocks += [Snake1d(d_model), WNConv1d(d_model, latent_dim, kernel_size=3, padding=1)]
         self.block = nn.Sequential(*blocks)
+        self.valid = False  # padding=False (CodecMixin.padding): unpadded convs
 
     def forward(self, x, return_feat: bool = False):
         if self.training:  # autograd path (vrvq_amd/train.py)
+            if self.valid:
+                raise NotImplementedError("padding=False is an inference (compress) mode")
             out, feat = train.encoder_forward(self, x)
+            return (out, feat) if return_feat else out
+        n = len(self.block)
+        if self.valid:
+            # Unpadded convs change every length, so the per-module forms run (Snake in each
+            # conv's prologue, residual units with the centre-cropped skip).
+            x = self.block[0](x)
+            for i in range(1, n - 2):
+                x = self.block[i](x)
+            out = self.block[n - 1](x, snake=self.block[n - 2])
+            # the unpadded k3 conv leaves z 2 frames shorter than feat: feat is centre-cropped
+            # to z's frames so the importance map gates the frames it was computed for
+            p = (x.shape[-1] - out.shape[-1]) // 2
+            feat = x[..., p:x.shape[-1] - p].contiguous() if p > 0 else x
             return (out, feat) if return_feat else out
         # Chained launches: every conv's epilogue also writes the next Snake's output, so each
         # activation is evaluated once per element (include/vrvq.h, producer-side Snake).
-        n = len(self.block)
         x, x_snk = self.block[0](x, out_snake=self.block[1].entry_snake())
         for i in range(1, n - 2):
             last = i == n - 3
@@ -64,11 +79,19 @@ class Decoder(nn.Module):
         layers += [Snake1d(output_dim), WNConv1d(output_dim, d_out, kernel_size=7, padding=3),
                    nn.Tanh()]
         self.model = nn.Sequential(*layers)
+        self.valid = False  # padding=False (CodecMixin.padding): unpadded convs
 
     def forward(self, x):
         if self.training:
+            if self.valid:
+                raise NotImplementedError("padding=False is an inference (decompress) mode")
             return train.decoder_forward(self, x)
         n = len(self.model)
+        if self.valid:
+            x = self.model[0](x)
+            for i in range(1, n - 3):
+                x = self.model[i](x)
+            return self.model[n - 2](x, snake=self.model[n - 3], epilogue=ops.EPI_TANH)
         _, x_snk = self.model[0](x, out_snake=self.model[1].entry_snake(), want_raw=False)
         for i in range(1, n - 3):
             nxt = self.model[n - 3] if i == n - 4 else self.model[i + 1].entry_snake()
@@ -341,30 +364,49 @@ class CodecMixin:
 
     @padding.setter
     def padding(self, value):
-        if not value:
-            raise NotImplementedError("padding=False windows belong to the chunked compress "
-                                      "path (SURVEY.md §8f row 4)")
-        self._padding = True
+        """models/dac_base.py:68-84: padding=False zeroes every encoder / decoder conv's padding
+        (kept in `original_padding`), True restores it. The importance subnet keeps its "same"
+        k3 padding: zeroed, its imp_map would be 12 frames shorter than z and the reference
+        fails at the mask product (models/quantize.py:421)."""
+        assert isinstance(value, bool)
+        for part in (self.encoder, self.decoder):
+            for layer in part.modules():
+                if not isinstance(layer, (WNConv1d, WNConvTranspose1d)):
+                    continue
+                if value:
+                    if hasattr(layer, "original_padding"):
+                        layer.padding = layer.original_padding
+                else:
+                    if not hasattr(layer, "original_padding") or layer.padding != (0,):
+                        layer.original_padding = layer.padding
+                    layer.padding = tuple(0 for _ in layer.padding)
+            part.valid = not value
+        self._padding = value
 
     def _conv_layers(self):
         return [m for m in self.modules() if isinstance(m, (WNConv1d, WNConvTranspose1d))]
 
-    @torch.no_grad()
     def compress(self, audio_path_or_signal, win_duration: float = 1.0, verbose: bool = False,
-                 normalize_db: float = -16, n_quantizers: int = None):
-        """models/dac_base.py:130-240 — raises NotImplementedError in the reference (:161)
-        before any work; kept identical for drop-in behaviour."""
-        raise NotImplementedError
+                 normalize_db: float = -16, n_quantizers: int = None, **kw):
+        """models/dac_base.py:130-240 (the body after the reference's NotImplementedError at
+        :161): chunked encode to a DACFile on the HIP path — vrvq_amd/codec.py."""
+        from .codec import compress
+        return compress(self, audio_path_or_signal, win_duration, verbose, normalize_db,
+                        n_quantizers, **kw)
 
-    @torch.no_grad()
-    def decompress(self, obj, verbose: bool = False):
-        """models/dac_base.py:243-304 — raises NotImplementedError in the reference (:264)."""
-        raise NotImplementedError
+    def decompress(self, obj, verbose: bool = False, **kw):
+        """models/dac_base.py:243-304 (after the reference's raise at :264): DACFile -> audio
+        (vrvq_amd/codec.py)."""
+        from .codec import decompress
+        return decompress(self, obj, verbose, **kw)
 
-    def get_delay(self):
-        l_out = self.get_output_length(0)
+    def get_delay(self, layers=None):
+        """models/dac_base.py:86-110 over every conv in self.modules() (as the reference), or
+        over `layers`."""
+        layers = self._conv_layers() if layers is None else layers
+        l_out = self.get_output_length(0, layers)
         L = l_out
-        for layer in reversed(self._conv_layers()):
+        for layer in reversed(layers):
             d, k, s = layer.dilation[0], layer.kernel_size[0], layer.stride[0]
             if isinstance(layer, WNConvTranspose1d):
                 L = ((L - d * (k - 1) - 1) / s) + 1
@@ -373,9 +415,10 @@ class CodecMixin:
             L = math.ceil(L)
         return (L - l_out) // 2
 
-    def get_output_length(self, input_length):
+    def get_output_length(self, input_length, layers=None):
+        """models/dac_base.py:112-127."""
         L = input_length
-        for layer in self._conv_layers():
+        for layer in (self._conv_layers() if layers is None else layers):
             d, k, s = layer.dilation[0], layer.kernel_size[0], layer.stride[0]
             if isinstance(layer, WNConv1d):
                 L = ((L - d * (k - 1) - 1) / s) + 1
@@ -383,6 +426,15 @@ class CodecMixin:
                 L = (L - 1) * s + d * (k - 1) + 1
             L = math.floor(L)
         return L
+
+    def codec_layers(self):
+        """The convs a chunked window passes through: encoder then decoder. The reference's
+        get_delay / get_output_length also walk the quantizer (its importance subnet's six k3
+        convs take 12 frames = 6144 samples off the length and 3072 off the delay), which
+        would misplace every window of a VBR model; for a CBR model the two lists give the
+        same numbers."""
+        return [m for part in (self.encoder, self.decoder) for m in part.modules()
+                if isinstance(m, (WNConv1d, WNConvTranspose1d))]
 
 
 class DAC_VRVQ(nn.Module, CodecMixin):

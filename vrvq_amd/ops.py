@@ -63,8 +63,8 @@ def conv_out_len(tin: int, k: int, stride: int, pad: int, dil: int) -> int:
     return (tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
 
 
-def convt_out_len(tin: int, stride: int) -> int:
-    p = (stride + 1) // 2
+def convt_out_len(tin: int, stride: int, pad: int = -1) -> int:
+    p = (stride + 1) // 2 if pad < 0 else pad
     return (tin - 1) * stride - 2 * p + 2 * stride
 
 
@@ -117,11 +117,12 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
                      alpha: Optional[torch.Tensor] = None,
                      inv_alpha: Optional[torch.Tensor] = None,
                      out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                     want_raw: bool = True):
-    """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d."""
+                     want_raw: bool = True, pad: int = -1):
+    """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d. pad -1 is
+    the DecoderBlock's ceil(stride / 2), 0 the padding=False window of the chunked codec."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv_transpose1d(x, w_packed, int(cout), int(stride), bias, alpha,
-                                          inv_alpha, ao, io, bool(want_raw))
+                                          inv_alpha, ao, io, bool(want_raw), int(pad))
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -318,9 +319,10 @@ def _register_fakes():
         return pair(x, (B, cout, tout), alpha_out, want_raw)
 
     @reg("vrvq::snake_conv_transpose1d")
-    def _(x, w_packed, cout, stride, bias, alpha, inv_alpha, alpha_out, inv_alpha_out, want_raw):
+    def _(x, w_packed, cout, stride, bias, alpha, inv_alpha, alpha_out, inv_alpha_out, want_raw,
+          pad=-1):
         B, _c, tin = x.shape
-        return pair(x, (B, cout, convt_out_len(tin, stride)), alpha_out, want_raw)
+        return pair(x, (B, cout, convt_out_len(tin, stride, pad)), alpha_out, want_raw)
 
     @reg("vrvq::residual_unit")
     def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw):
