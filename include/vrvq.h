@@ -85,10 +85,21 @@ int vrvq_codebook_prep(const float* cb, int rows, int dim, float* cbn, float* c2
  * NULL when only the activated tensor is needed (it must not be NULL otherwise).
  * ------------------------------------------------------------------------------------- */
 int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
-                const float* inv_alpha, const float* w_packed, int cout, int cout_pad, int k,
+                const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
+                int cout_pad, int k,
                 int stride, int pad, int dil, const float* bias, const float* residual,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
+
+/* fp32 convolution on the bf16 matrix cores (the "x3" path, vrvq_amd/csrc/conv_x3.h): with
+ * w_x3 = vrvq_pack_x3_weight(w_packed) (null: the fp32-input MFMA path) the stride-1 convs
+ * (k in {1, 2, 3, 7}; also the ConvTranspose1d and the ResidualUnit's k7) split both operands
+ * exactly into three bf16 terms and accumulate the six products >= 2^-16 of each fp32
+ * product in fp32 — fp32 accuracy at 2.7x the MFMA ceiling. Strided convs ignore w_x3.
+ * vrvq_x3_weight_size gives the buffer length in uint16 elements. */
+int vrvq_x3_weight_size(int cin, int k, int cout_pad, long long* n_u16);
+int vrvq_pack_x3_weight(const float* w_packed, int cin, int k, int cout_pad, uint16_t* w_x3,
+                        vrvq_stream_t stream);
 
 /* Pack a folded Conv1d weight w[Cout][Cin][k] into [Cin][k][cout_pad]. */
 int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
@@ -103,7 +114,8 @@ int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_p
  * vrvq_pack_conv1d_weight (same cout_pad). Supported: C in {64, 96, 128, 192, 256}, dil <= 9;
  * other C return VRVQ_ERR_UNSUPPORTED (callers use the two-launch form). */
 int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels, int frames,
-                       int dil, const float* w7_packed, const float* b7, const float* alpha2,
+                       int dil, const float* w7_packed, const uint16_t* w7_x3, const float* b7,
+                       const float* alpha2,
                        const float* inv_alpha2, const float* w1_packed, const float* b1,
                        int cout_pad, float* y, const float* alpha_out,
                        const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
@@ -126,7 +138,8 @@ int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin, const flo
  * (tin - 1)*stride - 2*pad + 2*stride. pad = 0 is the padding=False window of the chunked
  * codec (CodecMixin.padding setter, models/dac_base.py:68-84: every conv's padding -> 0). */
 int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int tin, const float* alpha,
-                              const float* inv_alpha, const float* w_packed, int cout,
+                              const float* inv_alpha, const float* w_packed,
+                              const uint16_t* w_x3, int cout,
                               int cout_pad, int stride, int pad, const float* bias, float* y,
                               const float* alpha_out, const float* inv_alpha_out,
                               float* y_snake, vrvq_stream_t stream);

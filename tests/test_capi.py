@@ -56,8 +56,8 @@ def test_argument_errors_raise_before_launch():
     lib = _lib.load()
     # null pointers -> VRVQ_ERR_ARG, returned by the host-side check (no GPU touched)
     assert lib.vrvq_weight_norm(None, None, 4, 4, None, None) == 10001
-    assert lib.vrvq_conv1d(None, 1, 1, 8, None, None, None, 1, 128, 3, 1, 1, 1, None, None, 0,
-                           None, 8, None, None, None, None) == 10001
+    assert lib.vrvq_conv1d(None, 1, 1, 8, None, None, None, None, 1, 128, 3, 1, 1, 1, None,
+                           None, 0, None, 8, None, None, None, None) == 10001
     assert lib.vrvq_rvq_encode(*([None] + [1] * 6 + [None] * 10 + [1.0] + [None] * 7 +
                                  [0, None])) == 10001
     n = ctypes.c_longlong(0)
@@ -67,8 +67,12 @@ def test_argument_errors_raise_before_launch():
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
     # geometry mismatch (tout inconsistent with the conv formula)
     p = ctypes.c_void_p(16)
-    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, 4, 128, 7, 1, 3, 1, None, None, 0,
-                           p, 99, None, None, None, None) == 10001
+    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, None, 4, 128, 7, 1, 3, 1, None, None,
+                           0, p, 99, None, None, None, None) == 10001
     # producer-side snake without its alpha
-    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, 4, 128, 7, 1, 3, 1, None, None, 0,
-                           None, 100, None, None, p, None) == 10001
+    assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, None, 4, 128, 7, 1, 3, 1, None, None,
+                           0, None, 100, None, None, p, None) == 10001
+    # x3 weight size: chunks x 3 planes x padded octets x cout_pad x 8 bf16
+    assert lib.vrvq_x3_weight_size(384, 7, 384, ctypes.byref(n)) == 0
+    assert n.value == 48 * 3 * 8 * 384 * 8
+    assert lib.vrvq_x3_weight_size(384, 5, 384, ctypes.byref(n)) == 10002

@@ -243,6 +243,60 @@ def test_conv_transpose1d_vs_torch(case):
     assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
 
 
+X3_CONV_CASES = [c for c in CONV_CASES if c[5] == 1 and c[4] in (1, 3, 7) and c[1] >= 8]
+
+
+@pytest.mark.parametrize("case", X3_CONV_CASES)
+def test_conv1d_x3_vs_torch(case):
+    """The bf16x3 split MFMA path (csrc/conv_x3.h) against torch fp64, at the fp32 path's
+    tolerance, and its error no larger than a small multiple of the fp32 MFMA path's."""
+    B, cin, cout, T, k, s, p, d, use_snake, use_res, epi = case
+    gen = torch.Generator(device="cpu").manual_seed(hash(case) & 0xFFFF)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cout, cin, k, generator=gen) / np.sqrt(cin * k)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    tout = (T + 2 * p - d * (k - 1) - 1) // s + 1
+    res = (torch.randn(B, cout, tout, generator=gen)).to(DEV) if use_res else None
+    xin = _snake_ref(x, alpha) if use_snake else x
+    ref = F.conv1d(xin.double(), w.double(), b.double(), stride=s, padding=p, dilation=d)
+    if use_res:
+        ref = res.double() + ref
+    ref = [ref, torch.tanh(ref), torch.sigmoid(ref)][epi].cpu().numpy()
+    wp, cout_pad = ops.pack_conv1d_weight(w)
+    w3 = ops.pack_x3_weight(wp, k)
+    kw = dict(bias=b, alpha=alpha if use_snake else None,
+              inv_alpha=ops.snake_inv_alpha(alpha) if use_snake else None, residual=res,
+              epilogue=epi)
+    y32 = ops.conv1d(x, wp, cout, cout_pad, k, s, p, d, **kw)
+    y3 = ops.conv1d(x, wp, cout, cout_pad, k, s, p, d, w_x3=w3, **kw)
+    e32 = rel_err(y32.cpu().numpy(), ref)
+    e3 = rel_err(y3.cpu().numpy(), ref)
+    assert e3 < 1e-5
+    assert e3 <= 4 * e32 + 2e-7, (e3, e32)
+
+
+@pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8),
+                                  (2, 384, 192, 333, 4), (2, 192, 96, 1000, 2),
+                                  (1, 16, 8, 1, 2), (2, 64, 40, 77, 3)])
+def test_conv_transpose1d_x3_vs_torch(case):
+    B, cin, cout, T, s = case
+    gen = torch.Generator(device="cpu").manual_seed(s * 1000 + T + 1)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cin, cout, 2 * s, generator=gen) / np.sqrt(cin * 2)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    ref = F.conv_transpose1d(_snake_ref(x, alpha).double(), w.double(), b.double(), stride=s,
+                             padding=(s + 1) // 2).cpu().numpy()
+    wp, cout_pad = ops.pack_convt1d_weight(w, s)
+    w3 = ops.pack_x3_weight(wp, 2)
+    kw = dict(bias=b, alpha=alpha, inv_alpha=ops.snake_inv_alpha(alpha))
+    e32 = rel_err(ops.conv_transpose1d(x, wp, cout, cout_pad, s, **kw).cpu().numpy(), ref)
+    e3 = rel_err(ops.conv_transpose1d(x, wp, cout, cout_pad, s, w_x3=w3, **kw).cpu().numpy(), ref)
+    assert e3 < 1e-5
+    assert e3 <= 4 * e32 + 2e-7, (e3, e32)
+
+
 def test_conv_transpose1d_unsupported_stride_raises():
     """Strides whose phase rows cannot tile 128 or 192 rows (5, 7) are rejected, not computed
     wrong (the epilogue maps whole output channels per tile)."""
@@ -517,7 +571,9 @@ def test_residual_unit_fused_vs_two_launch(C, T, dil, want_raw):
     # C = 192 at T > 96, where the two-launch k7 also uses a 192-row tile). For C = 256, and
     # C = 192 at T <= 96, the two-launch k7 runs 128-row tiles with 8-channel K chunks against
     # the fused kernel's 4: a different fp32 summation order, compared at 1e-6.
-    if C > 192 or (C == 192 and T <= 96):
+    # With the x3 path on, the two-launch k1 runs on the split bf16 MFMA and the fused
+    # kernel's phase 2 on the fp32 MFMA: same sums, another rounding, compared at 1e-6.
+    if ops.X3 or C > 192 or (C == 192 and T <= 96):
         assert rel_err(ys_f.cpu().numpy(), ys_2.cpu().numpy()) < 1e-6
     else:
         assert torch.equal(ys_f, ys_2)

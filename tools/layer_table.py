@@ -22,7 +22,8 @@ CALLS = []
 
 def _fake():
     def conv1d(x, wp, cout, cout_pad, k, stride=1, pad=0, dil=1, bias=None, alpha=None,
-               inv_alpha=None, residual=None, epilogue=0, out_snake=None, want_raw=True):
+               inv_alpha=None, residual=None, epilogue=0, out_snake=None, want_raw=True,
+               w_x3=None):
         B, cin, tin = x.shape
         tout = (tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
         CALLS.append(("conv", cin, cout, k, stride, dil, tout, B,
@@ -31,7 +32,7 @@ def _fake():
         return y if out_snake is None else (y, torch.empty_like(y))
 
     def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None,
-              out_snake=None, want_raw=True):
+              out_snake=None, want_raw=True, pad=-1, w_x3=None):
         B, cin, tin = x.shape
         CALLS.append(("convT", cin, cout, 2 * stride, stride, 1, tin * stride, B,
                       2.0 * B * cin * cout * tin * 2 * stride, False))
@@ -39,7 +40,7 @@ def _fake():
         return y if out_snake is None else (y, torch.empty_like(y))
 
     def residual_unit(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad,
-                      out_snake=None, want_raw=True):
+                      out_snake=None, want_raw=True, w7_x3=None):
         B, C, T = x.shape
         CALLS.append(("RU", C, C, 7, 1, dil, T, B, 2.0 * B * C * T * C * 8, True))
         y = torch.empty(B, C, T)
@@ -52,6 +53,7 @@ def _fake():
     ops.snake_inv_alpha = lambda a: a
     ops.pack_conv1d_weight = lambda w: (w, 128)
     ops.pack_convt1d_weight = lambda w, s: (w, 128)
+    ops.pack_x3_weight = lambda w, k: w
     ops.codebook_prep = lambda cb: (cb, cb[..., 0])
 
     def rvq_codes(z, w_in_t, b_in, cb, cbn, c2, w_out, b_out):

@@ -22,14 +22,16 @@ SIGNATURES = {
     "vrvq_weight_norm": [_P, _P, _I, _I, _P, _P],
     "vrvq_snake_inv_alpha": [_P, _I, _P, _P],
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
-    "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
+    "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
+    "vrvq_x3_weight_size": [_I, _I, _I, _P],
+    "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
-    "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P,
-                           _P],
+    "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
+                           _P, _P],
     "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
-    "vrvq_conv_transpose1d_pad": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P,
-                                  _P],
+    "vrvq_conv_transpose1d_pad": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
+                                  _P, _P],
     "vrvq_pack_convt1d_weight": [_P, _I, _I, _I, _I, _P, _P],
     "vrvq_rvq_cross_prep": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
     "vrvq_rvq_frag": [_P, _I, _I, _I, _P, _P],

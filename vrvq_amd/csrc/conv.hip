@@ -16,19 +16,29 @@
 // models/importance_subnet.py:38-45.
 #include "common.h"
 #include "conv_core.h"
+#include "conv_x3.h"
 #include <stdlib.h>
 
 namespace {
 
 using namespace vrvq_conv;
 
-template <int BM, int BN, int WM, int NW, int KS>
+template <int BM, int BN, int WM, int NW, int KS, bool X3>
 __global__ __launch_bounds__(64 * NW) void conv_mfma_kernel(ConvArgs a) {
   using TC = TileCfg<BM, BN, WM, NW>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
-  const int mt = bid % a.n_mt;
-  bid /= a.n_mt;
+  int mt;
+  if (a.mt_slow) {
+    // M tile slowest: the workgroups in flight (a window of consecutive ids, spread over the 8
+    // XCDs) all use one weight tile, so each XCD's L2 holds it instead of every M tile's
+    const int per = (int)gridDim.x / a.n_mt;
+    mt = bid / per;
+    bid -= mt * per;
+  } else {
+    mt = bid % a.n_mt;
+    bid /= a.n_mt;
+  }
   const int nt = bid % a.n_nt;
   const int b = bid / a.n_nt;
   const int m0 = mt * BM;
@@ -40,7 +50,8 @@ __global__ __launch_bounds__(64 * NW) void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TC::RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
+  else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
 }
 
@@ -230,6 +241,35 @@ int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
   return vrvq_launch_status();
 }
 
+// tuning override: VRVQ_CONV_MTSLOW=1 (M tile slowest) | 0 (default: 495.1 vs 492.6
+// audio-sec/s with it, profiles/r02zd_conv_ab.txt — the weight tiles are not what limits)
+static int conv_mt_slow() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_MTSLOW");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// Where the bf16x3 path runs when a pre-split weight is given (VRVQ_CONV_X3_RULE=0: every
+// eligible tile). Measured per layer at B = 32 (profiles/r02zd_x3_layers.txt, fp32 -> x3):
+// 384 k7 128x128 3.32 -> 2.55 ms, ConvT 1536->768 1.27 -> 0.69 ms, ConvT 384->192 2.16 ->
+// 1.64 ms, 768 k7 192x64 1.80 -> 1.70 ms, 512 k1 -25 %; the one loss is the 192x64 k = 1
+// tile (768 k1 + skip 0.34 -> 0.37 ms), which keeps the fp32 path.
+static int x3_rule() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_X3_RULE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
+  (void)a;
+  if (x3_rule() == 0) return true;
+  return !(ks == 1 && bm == 192 && bn == 64);
+}
+
 template <int BM, int BN, int WM, int NW, int KS>
 int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   ConvArgs a = a0;
@@ -243,20 +283,38 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
   const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
   const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
+  const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
+  const long long nblk = (long long)a.n_mt * a.n_nt * batch;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  // bf16x3 split path (conv_x3.h): stride-1 windows, a pre-split weight, the stage in LDS
+  a.mt_slow = conv_mt_slow();
+  if constexpr (NW == 4 && BM <= 192 && (KS == 1 || KS == 2 || KS == 3 || KS == 7)) {
+    constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
+    size_t lx = x3_lds_bytes<KS, BM>(XW);
+    if (lx < epi) lx = epi;
+    if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
+        x3_tile_ok(BM, BN, KS, a)) {
+      if (lx > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
+        if (e != hipSuccess) return (int)e;
+      }
+      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true>), dim3((unsigned)nblk),
+                         dim3(64 * NW), lx, st, a);
+      return vrvq_launch_status();
+    }
+  }
   if (XW > 64 * WinCfg<KS, BN>::PER_ROW) return VRVQ_ERR_UNSUPPORTED;  // window > staged lanes
   size_t lds = 2 * (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
-  const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
   if (lds < epi) lds = epi;  // epilogue tile
   if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  const long long nblk = (long long)a.n_mt * a.n_nt * batch;
-  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS>), dim3((unsigned)nblk), dim3(64 * NW),
-                     lds, st, a);
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, false>), dim3((unsigned)nblk),
+                     dim3(64 * NW), lds, st, a);
   return vrvq_launch_status();
 }
 
@@ -421,10 +479,81 @@ __global__ void pack_convt1d_kernel(const float* __restrict__ w, int cin, int co
   }
 }
 
+// Pre-split weight for the x3 mainloop (conv_x3.h): from the fp32 packed layout
+// wp[ci][tap][m_pad] (WNConv1d; the polyphase ConvTranspose1d layout is the same with 2 taps)
+// to w3[chunk][plane][octet][m_pad][8] bf16, octet o = tap * CK/8 + channel octet (zero for
+// the padding octet and channels >= cin).
+template <int KS>
+__global__ void pack_x3_kernel(const float* __restrict__ wp, int cin, int m_pad,
+                               u32x4* __restrict__ w3, size_t total) {
+  using XC = X3Cfg<KS>;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i % m_pad);
+    size_t r = i / m_pad;
+    const int o = (int)(r % XC::NO2);
+    r /= XC::NO2;
+    const int plane = (int)(r % 3);
+    const int chunk = (int)(r / 3);
+    const int tap = o / XC::NC8, c8 = o - tap * XC::NC8;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ci = chunk * XC::CK + c8 * 8 + u;
+      v[u] = (o < XC::NO && ci < cin) ? wp[((size_t)ci * KS + tap) * m_pad + m] : 0.0f;
+    }
+    unsigned h[4], mm[4], l[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) split3x2(v[2 * u], v[2 * u + 1], h[u], mm[u], l[u]);
+    w3[i] = plane == 0 ? u32x4{h[0], h[1], h[2], h[3]}
+          : plane == 1 ? u32x4{mm[0], mm[1], mm[2], mm[3]} : u32x4{l[0], l[1], l[2], l[3]};
+  }
+}
+
+static long long x3_size_u16(int cin, int k, int m_pad) {
+  auto sz = [&](int ck, int no2) {
+    return (long long)((cin + ck - 1) / ck) * 3 * no2 * m_pad * 8;
+  };
+  switch (k) {
+    case 1: return sz(X3Cfg<1>::CK, X3Cfg<1>::NO2);
+    case 2: return sz(X3Cfg<2>::CK, X3Cfg<2>::NO2);
+    case 3: return sz(X3Cfg<3>::CK, X3Cfg<3>::NO2);
+    case 7: return sz(X3Cfg<7>::CK, X3Cfg<7>::NO2);
+    default: return -1;
+  }
+}
+
 }  // namespace
 
+extern "C" int vrvq_x3_weight_size(int cin, int k, int cout_pad, long long* n_u16) {
+  VRVQ_CHECK_ARG(n_u16 && cin > 0 && cout_pad > 0);
+  const long long n = x3_size_u16(cin, k, cout_pad);
+  if (n < 0) return VRVQ_ERR_UNSUPPORTED;
+  *n_u16 = n;
+  return 0;
+}
+
+extern "C" int vrvq_pack_x3_weight(const float* w_packed, int cin, int k, int cout_pad,
+                                   uint16_t* w_x3, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w_packed && w_x3 && cin > 0 && cout_pad > 0);
+  const long long n = x3_size_u16(cin, k, cout_pad);
+  if (n < 0) return VRVQ_ERR_UNSUPPORTED;
+  const size_t total = (size_t)n / 8;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  u32x4* out = reinterpret_cast<u32x4*>(w_x3);
+  hipStream_t st = as_stream(stream);
+  switch (k) {
+    case 1: hipLaunchKernelGGL(pack_x3_kernel<1>, dim3(grid), dim3(256), 0, st, w_packed, cin, cout_pad, out, total); break;
+    case 2: hipLaunchKernelGGL(pack_x3_kernel<2>, dim3(grid), dim3(256), 0, st, w_packed, cin, cout_pad, out, total); break;
+    case 3: hipLaunchKernelGGL(pack_x3_kernel<3>, dim3(grid), dim3(256), 0, st, w_packed, cin, cout_pad, out, total); break;
+    default: hipLaunchKernelGGL(pack_x3_kernel<7>, dim3(grid), dim3(256), 0, st, w_packed, cin, cout_pad, out, total); break;
+  }
+  return vrvq_launch_status();
+}
+
 extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
-                           const float* inv_alpha, const float* w_packed, int cout,
+                           const float* inv_alpha, const float* w_packed,
+                           const uint16_t* w_x3, int cout,
                            int cout_pad, int k, int stride, int pad, int dil, const float* bias,
                            const float* residual, int epilogue, float* y, int tout,
                            const float* alpha_out, const float* inv_alpha_out, float* y_snake,
@@ -448,6 +577,7 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   if (stride > 1 && (stride & (stride - 1)) == 0)
     while ((1 << a.ssh) < stride) ++a.ssh;
   a.ylen = tout; a.epi = epilogue;
+  a.w3 = reinterpret_cast<const unsigned*>(w_x3);
   if (cout <= SMALL_COUT && stride == 1 && cin * k * (cout == 1 ? 1 : SMALL_COUT) <= SMALL_WMAX)
     return launch_small(a, batch, k, as_stream(stream));
   return dispatch_ks(k, a, batch, as_stream(stream));
@@ -460,14 +590,15 @@ extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin
                                      const float* inv_alpha_out, float* y_snake,
                                      vrvq_stream_t stream) {
   // math.ceil(stride / 2), models/layers.py:102
-  return vrvq_conv_transpose1d_pad(x, batch, cin, tin, alpha, inv_alpha, w_packed, cout,
-                                   cout_pad, stride, (stride + 1) / 2, bias, y, alpha_out,
+  return vrvq_conv_transpose1d_pad(x, batch, cin, tin, alpha, inv_alpha, w_packed, nullptr,
+                                   cout, cout_pad, stride, (stride + 1) / 2, bias, y, alpha_out,
                                    inv_alpha_out, y_snake, stream);
 }
 
 extern "C" int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int tin,
                                          const float* alpha, const float* inv_alpha,
-                                         const float* w_packed, int cout, int cout_pad,
+                                         const float* w_packed, const uint16_t* w_x3,
+                                         int cout, int cout_pad,
                                          int stride, int pad, const float* bias, float* y,
                                          const float* alpha_out, const float* inv_alpha_out,
                                          float* y_snake, vrvq_stream_t stream) {
@@ -487,6 +618,7 @@ extern "C" int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int
   a.stride = 1; a.pad = 1; a.dil = 1; a.ng = tin + 1; a.up = stride; a.up_pad = p;
   a.ylen = (tin - 1) * stride - 2 * p + 2 * stride;
   a.epi = VRVQ_EPI_NONE;
+  a.w3 = reinterpret_cast<const unsigned*>(w_x3);
   return dispatch_ks(2, a, batch, as_stream(stream));
 }
 

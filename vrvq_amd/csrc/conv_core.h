@@ -31,6 +31,8 @@ struct ConvArgs {
   int ylen;                // output row length
   int epi;
   int n_mt, n_nt;          // M tiles, N tiles
+  const unsigned* w3;      // pre-split bf16 weight planes (conv_x3.h) or null: fp32 MFMA path
+  int mt_slow;             // block order: M tile slowest (all CUs on one weight tile: L2 reuse)
 };
 
 template <int KS, int BM, int BN>

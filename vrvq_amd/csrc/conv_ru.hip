@@ -16,6 +16,8 @@
 // 768-channel units (T = 696) use the two-launch form.
 #include "common.h"
 #include "conv_core.h"
+#include "conv_x3.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -31,7 +33,7 @@ struct RuArgs {
   int C;
 };
 
-template <int BM, int BN, int WM, int NW>
+template <int BM, int BN, int WM, int NW, bool X3>
 __global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
   using TC = TileCfg<BM, BN, WM, NW>;
   constexpr int RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
@@ -52,7 +54,9 @@ __global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
     for (int j = 0; j < RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  conv_mainloop<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);  // ends with a barrier
+  // phase 1 on the bf16x3 split path when a pre-split W7 is given (conv_x3.h)
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);
+  else conv_mainloop<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);  // ends with a barrier
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -118,6 +122,19 @@ __global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
   conv_epilogue<BM, BN, WM, NW>(ra.p2, smem, acc, b, 0, n0);
 }
 
+// Measured at B = 32 (profiles/r02zd_x3_layers.txt): the x3 phase 1 wins for C = 64
+// (1.17 -> 1.02 ms per unit) and C = 128 (1.95 -> 1.93 ms) and loses for C = 96 / 192
+// (+12 % to +23 %): its LDS stages leave room for one workgroup per CU (the fp32 kernels
+// run two or three), so nothing overlaps the fp32 phase 2 and the epilogue.
+// VRVQ_RU_X3=0: never, 1: C = 64 / 128 (default), 2: every C <= 192.
+static bool ru_x3_ok(int C) {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_RU_X3");
+    return e ? atoi(e) : 1;
+  }();
+  return v == 2 ? true : v == 1 ? (C == 64 || C == 128) : false;
+}
+
 template <int BM, int BN, int WM, int NW>
 int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   constexpr int CK = ChunkCfg<7, BM, BN>::CK;
@@ -135,23 +152,39 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
   if (lds < hsz) lds = hsz;
   if (lds < epi) lds = epi;
+  const long long nblk = (long long)a.n_nt * batch;
+  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  if constexpr (BM <= 192) {
+    size_t lx = x3_lds_bytes<7, BM>(XW);
+    if (lx < hsz) lx = hsz;
+    if (lx < epi) lx = epi;
+    if (a.w3 != nullptr && XW <= (BN - 1) + 6 * 9 + 1 && lx <= 160 * 1024 && ru_x3_ok(BM)) {
+      if (lx > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)ru_fused_kernel<BM, BN, WM, NW, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
+        if (e != hipSuccess) return (int)e;
+      }
+      hipLaunchKernelGGL((ru_fused_kernel<BM, BN, WM, NW, true>), dim3((unsigned)nblk),
+                         dim3(64 * NW), lx, st, ra);
+      return vrvq_launch_status();
+    }
+  }
   if (lds > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ru_fused_kernel<BM, BN, WM, NW>,
+    hipError_t e = hipFuncSetAttribute((const void*)ru_fused_kernel<BM, BN, WM, NW, false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  const long long nblk = (long long)a.n_nt * batch;
-  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-  hipLaunchKernelGGL((ru_fused_kernel<BM, BN, WM, NW>), dim3((unsigned)nblk), dim3(64 * NW), lds,
-                     st, ra);
+  hipLaunchKernelGGL((ru_fused_kernel<BM, BN, WM, NW, false>), dim3((unsigned)nblk),
+                     dim3(64 * NW), lds, st, ra);
   return vrvq_launch_status();
 }
 
 }  // namespace
 
 extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels,
-                                  int frames, int dil, const float* w7_packed, const float* b7,
+                                  int frames, int dil, const float* w7_packed,
+                                  const uint16_t* w7_x3, const float* b7,
                                   const float* alpha2, const float* inv_alpha2,
                                   const float* w1_packed, const float* b1, int cout_pad,
                                   float* y, const float* alpha_out, const float* inv_alpha_out,
@@ -168,6 +201,7 @@ extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch,
   p.cin = channels; p.tin = frames; p.M = channels; p.m_pad = cout_pad; p.cout = channels;
   p.stride = 1; p.pad = 3 * dil; p.dil = dil; p.ssh = 0; p.ng = frames; p.up = 0; p.up_pad = 0;
   p.ylen = frames; p.epi = VRVQ_EPI_NONE;
+  p.w3 = reinterpret_cast<const unsigned*>(w7_x3);
   ConvArgs& q = ra.p2;
   q = p;
   q.bias = b1; q.res = x; q.y = y; q.alpha_o = alpha_out; q.inv_alpha_o = inv_alpha_out;

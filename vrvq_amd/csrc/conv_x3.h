@@ -1,0 +1,257 @@
+// fp32 convolution on the bf16 matrix cores: the "x3" mainloop.
+//
+// gfx950 runs v_mfma_f32_32x32x16_bf16 at 16x the FLOP rate of the fp32-input
+// v_mfma_f32_32x32x2_f32 (32 vs 64 cycles for 8x the K). Every fp32 operand is split exactly
+// into three bf16 terms, v = h + m + l (round-to-nearest at each step: |m| <= 2^-8 |v|,
+// |l| <= 2^-16 |v|, and l is exact because a float has 24 significant bits), and a product
+// a*b is accumulated as the six terms whose size is >= 2^-16 |ab|:
+//     a_h b_h  +  (a_m b_m + a_h b_l + a_l b_h + a_h b_m + a_m b_h)
+// in fp32 (bf16 x bf16 products are exact in fp32). The dropped terms a_m b_l + a_l b_m +
+// a_l b_l are <= 2^-23 |ab|, the size of one fp32 rounding, so the result carries fp32
+// accuracy (tests compare it with the fp32 path and fp64). The h*h terms and the five
+// correction terms go to two accumulators that are added once at the end. 6 bf16 MFMAs per
+// 16 K (192 cycles) replace 8 fp32 MFMAs (512 cycles): 2.7x the MFMA ceiling.
+//
+// Operand layouts (32x32x16 bf16: lane l, r = l & 31, h = l >> 5 holds A[row r][k = 8h + e]
+// and B[k = 8h + e][col r], e = 0..7): K is ordered in "octets" of 8 consecutive input
+// channels at one tap; a K-chunk of CK channels has NO = KS * CK / 8 octets (tap-major),
+// padded to an even NO2 with zero weights, and MFMA step q takes octets (2q, 2q + 1) on the
+// two lane halves. Both operands are 16-byte LDS reads of one octet per plane:
+//     W stage  [plane][octet][BM rows][8]       (pre-split in HBM: vrvq_pack_x3_weight)
+//     X stage  [plane][CK/8][XWP positions][8]  (snake(x) split while staging)
+// The next K-chunk's W planes and x window are loaded into registers during the current
+// chunk's MFMAs (x: eight channels per position, split into three 16-byte planes at the store).
+#pragma once
+#include "conv_core.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+namespace vrvq_conv {
+
+template <int KS>
+struct X3Cfg {
+  static constexpr int CK = KS == 1 ? 32 : KS <= 3 ? 16 : 8;  // channels per K-chunk
+  static constexpr int NC8 = CK / 8;                        // channel octets per tap
+  static constexpr int NO = KS * NC8;                       // octets per chunk
+  static constexpr int NO2 = (NO + 1) & ~1;                 // padded to MFMA steps
+  static constexpr int NSTEP = NO2 / 2;
+};
+
+// Three planes of two floats (RNE at each step): v = h + m + l exactly.
+__device__ __forceinline__ void split3x2(float v0, float v1, unsigned& h, unsigned& m,
+                                         unsigned& l) {
+  const f32x2 v = {v0, v1};
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+  const f32x2 hf = {__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+  const f32x2 r = v - hf;
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+  const f32x2 mf = {__uint_as_float(mu << 16), __uint_as_float(mu & 0xffff0000u)};
+  const f32x2 s = r - mf;
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2));
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// LDS bytes of one pipeline stage.
+template <int KS, int BM>
+__host__ __device__ constexpr int x3_stage_w_bytes() {
+  return 3 * X3Cfg<KS>::NO2 * BM * 16;
+}
+__host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
+
+// W chunk staging through registers: uint4 u = tid + r*NT of the stage holds
+// (plane, octet, row) = (u / BM) -> w3[((chunk*3 + plane)*NO2 + octet)*m_pad + m0 + row].
+// Plain global loads (not LDS-DMA): the compiler then places the wait for them right before
+// the ds_write after the chunk's MFMAs; with LDS-DMA in inline asm it cannot see the loads and
+// its conservative waits at the next global load exposed their whole latency every chunk.
+template <int KS, int BM, int NT>
+struct X3W {
+  static constexpr int TOTAL = 3 * X3Cfg<KS>::NO2 * BM;  // uint4 per stage
+  static constexpr int WQ = (TOTAL + NT - 1) / NT;         // per thread
+};
+
+// K loop of the implicit GEMM on the split operands. Same contract as conv_mainloop (acc zero
+// on entry, holds W * Xs of the tile on exit, ends after a barrier with every LDS stage free);
+// stride-1 windows only (a.ssh == 0), a.w3 = the pre-split weight.
+template <int BM, int BN, int WM, int NW, int KS>
+__device__ __forceinline__ void conv_mainloop_x3(
+    const ConvArgs& a, float* smem,
+    f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
+    int n0) {
+  using TC = TileCfg<BM, BN, WM, NW>;
+  using XC = X3Cfg<KS>;
+  constexpr int NT = TC::NT, RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
+  constexpr int CK = XC::CK, NC8 = XC::NC8, NO = XC::NO, NO2 = XC::NO2, NSTEP = XC::NSTEP;
+  constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
+  constexpr int XI = (NC8 * XW_MAX + NT - 1) / NT;  // x items (octet, position) per thread
+  constexpr int WB = x3_stage_w_bytes<KS, BM>();
+
+  const int XW = (BN - 1) + (KS - 1) * a.dil + 1;
+  const int XWP = x3_xwp(XW);
+  const int STG = WB + 3 * NC8 * XWP * 16;  // bytes per stage
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const u32x4* w3 = reinterpret_cast<const u32x4*>(a.w3);
+  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  const int xbase = n0 - a.pad;
+  const int nitems = NC8 * XW;
+  char* sbase = reinterpret_cast<char*>(smem);
+
+  f32x16 accl[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accl[i][j][r] = 0.0f;
+
+  constexpr int WQ = X3W<KS, BM, NT>::WQ, WTOT = X3W<KS, BM, NT>::TOTAL;
+  u32x4 wr[WQ];
+  auto load_w = [&](int chunk) {
+#pragma unroll
+    for (int r = 0; r < WQ; ++r) {
+      const int u = min(tid + r * NT, WTOT - 1);  // clamped: no conditional load
+      const int po = u / BM, row = u - po * BM;
+      wr[r] = w3[((size_t)chunk * 3 * NO2 + po) * a.m_pad + m0 + row];
+    }
+  };
+  auto store_w = [&](char* stg) {
+    u32x4* ws = reinterpret_cast<u32x4*>(stg);
+#pragma unroll
+    for (int r = 0; r < WQ; ++r)
+      if (WTOT % NT == 0 || tid + r * NT < WTOT) ws[tid + r * NT] = wr[r];
+  };
+  float xr[XI][8];
+  // Branch-free loads from clamped addresses, kept raw: the zeroing select outside the window
+  // / input runs in store_x, after the MFMAs. (A select here makes the wave wait for the
+  // load before the chunk's MFMAs, and vmcnt retires in order, so that wait also covers the
+  // W DMA issued before it: the whole memory latency exposed once per chunk.)
+  auto load_x = [&](int ci0) {
+#pragma unroll
+    for (int it = 0; it < XI; ++it) {
+      const int e = tid + it * NT;
+      const int c8 = e / XW, pos = e - c8 * XW;
+      const int tc = min(max(xbase + pos, 0), a.tin - 1);
+      const int cb = ci0 + (e < nitems ? c8 : 0) * 8;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xr[it][u] = xb[(size_t)min(cb + u, a.cin - 1) * a.tin + tc];
+    }
+  };
+  auto store_x = [&](char* stg, int ci0) {
+    u32x4* xs = reinterpret_cast<u32x4*>(stg + WB);
+#pragma unroll
+    for (int it = 0; it < XI; ++it) {
+      const int e = tid + it * NT;
+      if (e >= nitems) continue;
+      const int c8 = e / XW, pos = e - c8 * XW;
+      const int t = xbase + pos;
+      const bool okp = t >= 0 && t < a.tin;
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (okp && ci0 + c8 * 8 + u < a.cin) ? xr[it][u] : 0.0f;
+      if (a.alpha != nullptr) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int ci = min(ci0 + c8 * 8 + u, a.cin - 1);
+          v[u] = snake_act(v[u], a.alpha[ci], a.inv_alpha[ci]);  // snake(0) = 0
+        }
+      }
+      unsigned h[4], m[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) split3x2(v[2 * u], v[2 * u + 1], h[u], m[u], l[u]);
+      xs[(0 * NC8 + c8) * XWP + pos] = u32x4{h[0], h[1], h[2], h[3]};
+      xs[(1 * NC8 + c8) * XWP + pos] = u32x4{m[0], m[1], m[2], m[3]};
+      xs[(2 * NC8 + c8) * XWP + pos] = u32x4{l[0], l[1], l[2], l[3]};
+    }
+  };
+
+  const int nchunks = (a.cin + CK - 1) / CK;
+  int cur = 0;
+  load_w(0);
+  load_x(0);
+  store_w(sbase);
+  store_x(sbase, 0);
+  __syncthreads();
+  const int col = wn * TN + lr;
+  for (int c = 0; c < nchunks; ++c) {
+    // Next chunk's loads in flight during this chunk's MFMAs. Unconditional (the last chunk
+    // reloads itself into the idle stage): under `if (more)` the compiler sinks the loads past
+    // the MFMAs into the store block, their only user.
+    const int cn = min(c + 1, nchunks - 1);
+    char* nxt = sbase + (cur ^ 1) * STG;
+    load_w(cn);
+    load_x(cn * CK);
+    __builtin_amdgcn_sched_barrier(0);
+    const u32x4* ws = reinterpret_cast<const u32x4*>(sbase + cur * STG);
+    const u32x4* xs = reinterpret_cast<const u32x4*>(sbase + cur * STG + WB);
+    auto rd = [&](int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
+      const int o = 2 * q + lh;
+      const int tap = o < NO ? o / NC8 : 0;  // padded octet: zero weights, any valid x
+      const int c8 = o - (o / NC8) * NC8;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < RM; ++i) av[p][i] = ws[(p * NO2 + o) * BM + wm * TM + i * 32 + lr];
+      const int xo = c8 * XWP + col + tap * a.dil;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bv[p][j] = xs[p * NC8 * XWP + xo + j * 32];
+    };
+    auto mma = [&](const u32x4 (&av)[3][RM], const u32x4 (&bv)[3][RN]) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          f32x16 t = accl[i][j];
+          t = mfma_bf16(av[1][i], bv[1][j], t);  // m m
+          t = mfma_bf16(av[0][i], bv[2][j], t);  // h l
+          t = mfma_bf16(av[2][i], bv[0][j], t);  // l h
+          t = mfma_bf16(av[0][i], bv[1][j], t);  // h m
+          t = mfma_bf16(av[1][i], bv[0][j], t);  // m h
+          accl[i][j] = t;
+          acc[i][j] = mfma_bf16(av[0][i], bv[0][j], acc[i][j]);  // h h
+        }
+    };
+    {
+      u32x4 a0[3][RM], b0[3][RN], a1[3][RM], b1[3][RN];
+      rd(0, a0, b0);
+#pragma unroll
+      for (int q = 0; q < NSTEP; q += 2) {
+        if (q + 1 < NSTEP) rd(q + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q + 2 < NSTEP) rd(q + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q + 1 < NSTEP) mma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    store_w(nxt);
+    store_x(nxt, cn * CK);
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = acc[i][j] + accl[i][j];
+}
+
+// LDS bytes the x3 mainloop needs for a window of XW positions.
+template <int KS, int BM>
+inline size_t x3_lds_bytes(int xw) {
+  return 2 * ((size_t)x3_stage_w_bytes<KS, BM>() + 3 * (size_t)X3Cfg<KS>::NC8 * x3_xwp(xw) * 16);
+}
+
+}  // namespace vrvq_conv

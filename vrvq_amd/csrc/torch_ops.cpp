@@ -132,6 +132,34 @@ Tensor pack_convt1d_weight(const Tensor& w, int64_t stride) {
   return wp;
 }
 
+// Pre-split bf16 weight planes for the x3 conv path (include/vrvq.h, vrvq_pack_x3_weight),
+// held as int16 storage. k = taps of the packed layout (2 for a polyphase ConvTranspose1d).
+Tensor pack_x3_weight(const Tensor& w_packed, int64_t k) {
+  check_t(w_packed, "w_packed");
+  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(1) == k,
+              "pack_x3_weight: w_packed must be (Cin, k, cout_pad)");
+  c10::DeviceGuard guard(w_packed.device());
+  const int64_t cin = w_packed.size(0), cout_pad = w_packed.size(2);
+  long long n = 0;
+  check_rc(vrvq_x3_weight_size((int)cin, (int)k, (int)cout_pad, &n), "vrvq_x3_weight_size");
+  Tensor w3 = at::empty({n}, w_packed.options().dtype(at::kShort));
+  check_rc(vrvq_pack_x3_weight(w_packed.data_ptr<float>(), (int)cin, (int)k, (int)cout_pad,
+                               reinterpret_cast<uint16_t*>(w3.data_ptr<int16_t>()),
+                               stream_of(w_packed)),
+           "vrvq_pack_x3_weight");
+  return w3;
+}
+
+const uint16_t* x3_ptr(const optional<Tensor>& w3, const Tensor& ref, int64_t cin, int64_t k,
+                       int64_t cout_pad) {
+  if (!w3.has_value()) return nullptr;
+  check_on(*w3, ref, "w_x3", at::kShort);
+  long long n = 0;
+  check_rc(vrvq_x3_weight_size((int)cin, (int)k, (int)cout_pad, &n), "vrvq_x3_weight_size");
+  TORCH_CHECK(w3->numel() == n, "w_x3: expected ", n, " elements (pack_x3_weight of w_packed)");
+  return reinterpret_cast<const uint16_t*>(w3->data_ptr<int16_t>());
+}
+
 // --------------------------------------------------------------------------- convs
 std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef shape,
                                             const optional<Tensor>& alpha_out,
@@ -161,7 +189,8 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
                                         const optional<Tensor>& inv_alpha,
                                         const optional<Tensor>& residual, int64_t epilogue,
                                         const optional<Tensor>& alpha_out,
-                                        const optional<Tensor>& inv_alpha_out, bool want_raw) {
+                                        const optional<Tensor>& inv_alpha_out, bool want_raw,
+                                        const optional<Tensor>& w_x3) {
   check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
@@ -181,8 +210,9 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
     TORCH_CHECK(residual->sizes() == at::IntArrayRef({B, cout, tout}),
                 "conv1d: residual shape must equal the output shape");
   auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  const uint16_t* w3 = x3_ptr(w_x3, x, cin, k, cout_pad);
   check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha), fp(inv_alpha),
-                       w_packed.data_ptr<float>(), (int)cout, (int)cout_pad, (int)k, (int)stride,
+                       w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad, (int)k, (int)stride,
                        (int)pad, (int)dil, fp(bias), fp(residual), (int)epilogue, opt_ptr(y),
                        (int)tout, fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
            "vrvq_conv1d");
@@ -194,7 +224,8 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
     const Tensor& x, const Tensor& w_packed, int64_t cout, int64_t stride,
     const optional<Tensor>& bias, const optional<Tensor>& alpha,
     const optional<Tensor>& inv_alpha, const optional<Tensor>& alpha_out,
-    const optional<Tensor>& inv_alpha_out, bool want_raw, int64_t pad) {
+    const optional<Tensor>& inv_alpha_out, bool want_raw, int64_t pad,
+    const optional<Tensor>& w_x3) {
   check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
@@ -212,8 +243,9 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
   const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
   const int64_t tout = (tin - 1) * stride - 2 * p + 2 * stride;
   auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  const uint16_t* w3 = x3_ptr(w_x3, x, cin, 2, w_packed.size(2));
   check_rc(vrvq_conv_transpose1d_pad(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                                     fp(inv_alpha), w_packed.data_ptr<float>(), (int)cout,
+                                     fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
                                      (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
                                      opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
                                      stream_of(x)),
@@ -227,7 +259,8 @@ std::tuple<Tensor, Tensor> residual_unit(const Tensor& x, const Tensor& x_snk, i
                                          const Tensor& alpha2, const Tensor& inv_alpha2,
                                          const Tensor& w1, const Tensor& b1,
                                          const optional<Tensor>& alpha_out,
-                                         const optional<Tensor>& inv_alpha_out, bool want_raw) {
+                                         const optional<Tensor>& inv_alpha_out, bool want_raw,
+                                         const optional<Tensor>& w7_x3) {
   check_t(x, "x");
   check_on(x_snk, x, "x_snk");
   check_on(w7, x, "w7");
@@ -245,7 +278,8 @@ std::tuple<Tensor, Tensor> residual_unit(const Tensor& x, const Tensor& x_snk, i
               "residual_unit: packed weights must be (C, 7, pad) and (C, 1, pad)");
   auto [y, ys, _u] = out_pair(x, {B, C, T}, alpha_out, inv_alpha_out, want_raw);
   check_rc(vrvq_residual_unit(x.data_ptr<float>(), x_snk.data_ptr<float>(), (int)B, (int)C,
-                              (int)T, (int)dil, w7.data_ptr<float>(), b7.data_ptr<float>(),
+                              (int)T, (int)dil, w7.data_ptr<float>(),
+                              x3_ptr(w7_x3, x, C, 7, w7.size(2)), b7.data_ptr<float>(),
                               alpha2.data_ptr<float>(), inv_alpha2.data_ptr<float>(),
                               w1.data_ptr<float>(), b1.data_ptr<float>(), (int)w7.size(2),
                               opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
@@ -823,18 +857,20 @@ TORCH_LIBRARY(vrvq, m) {
   m.def("codebook_prep(Tensor cb) -> (Tensor, Tensor)");
   m.def("pack_conv1d_weight(Tensor w) -> Tensor");
   m.def("pack_convt1d_weight(Tensor w, int stride) -> Tensor");
+  m.def("pack_x3_weight(Tensor w_packed, int k) -> Tensor");
   m.def(
       "snake_conv1d(Tensor x, Tensor w_packed, int cout, int stride, int pad, int dil, "
       "Tensor? bias, Tensor? alpha, Tensor? inv_alpha, Tensor? residual, int epilogue, "
-      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw) -> (Tensor, Tensor)");
+      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw, Tensor? w_x3=None) -> "
+      "(Tensor, Tensor)");
   m.def(
       "snake_conv_transpose1d(Tensor x, Tensor w_packed, int cout, int stride, Tensor? bias, "
       "Tensor? alpha, Tensor? inv_alpha, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw, int pad=-1) -> (Tensor, Tensor)");
+      "bool want_raw, int pad=-1, Tensor? w_x3=None) -> (Tensor, Tensor)");
   m.def(
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw) -> (Tensor, Tensor)");
+      "bool want_raw, Tensor? w7_x3=None) -> (Tensor, Tensor)");
   m.def("rvq_cross_prep(Tensor w_in_t, Tensor w_out, Tensor b_out) -> (Tensor, Tensor)");
   m.def("rvq_frag(Tensor cbn) -> Tensor");
   m.def(
@@ -891,6 +927,7 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("codebook_prep", &codebook_prep); \
   m.impl("pack_conv1d_weight", &pack_conv1d_weight); \
   m.impl("pack_convt1d_weight", &pack_convt1d_weight); \
+  m.impl("pack_x3_weight", &pack_x3_weight); \
   m.impl("snake_conv1d", &snake_conv1d); \
   m.impl("snake_conv_transpose1d", &snake_conv_transpose1d); \
   m.impl("residual_unit", &residual_unit); \

@@ -75,6 +75,7 @@ class WNConv1d(nn.Module):
         self.weight_g = nn.Parameter(g.reshape(out_channels, 1, 1).clone())
         self.weight_v = nn.Parameter(v)
         self._cache = None
+        self._cache_x3 = None
 
     def folded_weight(self) -> torch.Tensor:
         """w = v * (g / ||v||) in the reference layout (Cout, Cin, k)."""
@@ -86,6 +87,18 @@ class WNConv1d(nn.Module):
             wp, cout_pad = ops.pack_conv1d_weight(self.folded_weight())
             self._cache = (key, wp, cout_pad)
         return self._cache[1], self._cache[2]
+
+    def prepared_x3(self):
+        """bf16 planes of the packed weight for the x3 MFMA path (stride-1 k in {1, 3, 7} with
+        >= 8 input channels), or None (fp32-input MFMA path)."""
+        k = self.kernel_size[0]
+        if not (ops.X3 and self.stride[0] == 1 and k in ops.X3_TAPS and self.in_channels >= 8):
+            return None
+        wp, _ = self.prepared()
+        key = _param_key(self.weight_g, self.weight_v)
+        if self._cache_x3 is None or self._cache_x3[0] != key:
+            self._cache_x3 = (key, ops.pack_x3_weight(wp, k))
+        return self._cache_x3[1]
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
                 residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE,
@@ -101,7 +114,7 @@ class WNConv1d(nn.Module):
                           bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                           residual=residual, epilogue=epilogue,
                           out_snake=None if out_snake is None else out_snake.prepared(),
-                          want_raw=want_raw)
+                          want_raw=want_raw, w_x3=self.prepared_x3())
 
 
 class WNConvTranspose1d(nn.Module):
@@ -124,6 +137,7 @@ class WNConvTranspose1d(nn.Module):
         self.weight_g = nn.Parameter(g.reshape(in_channels, 1, 1).clone())
         self.weight_v = nn.Parameter(v)
         self._cache = None
+        self._cache_x3 = None
 
     def folded_weight(self) -> torch.Tensor:
         return ops.weight_norm(self.weight_g.detach().contiguous(), self.weight_v.detach().contiguous())
@@ -135,6 +149,16 @@ class WNConvTranspose1d(nn.Module):
             self._cache = (key, wp, cout_pad)
         return self._cache[1], self._cache[2]
 
+    def prepared_x3(self):
+        """bf16 planes of the polyphase weight (2 taps) for the x3 MFMA path, or None."""
+        if not (ops.X3 and self.in_channels >= 8):
+            return None
+        wp, _ = self.prepared()
+        key = _param_key(self.weight_g, self.weight_v)
+        if self._cache_x3 is None or self._cache_x3[0] != key:
+            self._cache_x3 = (key, ops.pack_x3_weight(wp, 2))
+        return self._cache_x3[1]
+
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
                 out_snake: Optional[Snake1d] = None, want_raw: bool = True):
         wp, cout_pad = self.prepared()
@@ -144,7 +168,8 @@ class WNConvTranspose1d(nn.Module):
         return ops.conv_transpose1d(x, wp, self.out_channels, cout_pad, self.stride[0],
                                     bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                                     out_snake=None if out_snake is None else out_snake.prepared(),
-                                    want_raw=want_raw, pad=self.padding[0])
+                                    want_raw=want_raw, pad=self.padding[0],
+                                    w_x3=self.prepared_x3())
 
 
 class ResidualUnit(nn.Module):
@@ -184,7 +209,8 @@ class ResidualUnit(nn.Module):
             return ops.residual_unit(x, x_snk, self.block[1].dilation[0], w7,
                                      self.block[1].bias.detach(), a2, ia2, w1,
                                      self.block[3].bias.detach(), cp7,
-                                     out_snake=out_snake.prepared(), want_raw=want_raw)
+                                     out_snake=out_snake.prepared(), want_raw=want_raw,
+                                     w7_x3=self.block[1].prepared_x3())
         return self.run_two_launch(x, x_snk, out_snake, want_raw)
 
     def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool):

@@ -98,17 +98,20 @@ def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k:
            stride: int = 1, pad: int = 0, dil: int = 1, bias: Optional[torch.Tensor] = None,
            alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
-           out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, want_raw: bool = True):
+           out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, want_raw: bool = True,
+           w_x3: Optional[torch.Tensor] = None):
     """y = epi(residual + conv1d(snake(x)) + bias) on the MFMA implicit-GEMM kernel.
 
     out_snake = (alpha_next, inv_alpha_next) also produces snake_next(y) from the epilogue
     (the next layer's Snake). Returns y, or (y | None, snake_next(y)) when out_snake is given
-    (y is None when want_raw is False)."""
+    (y is None when want_raw is False). w_x3 = pack_x3_weight(w_packed, k) selects the bf16x3
+    split MFMA path for stride-1 convs (include/vrvq.h)."""
     if w_packed.dim() != 3 or w_packed.shape[1] != k or w_packed.shape[2] != cout_pad:
         raise RuntimeError("conv1d: w_packed must be (Cin, k, cout_pad)")
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv1d(x, w_packed, int(cout), int(stride), int(pad), int(dil), bias,
-                                alpha, inv_alpha, residual, int(epilogue), ao, io, bool(want_raw))
+                                alpha, inv_alpha, residual, int(epilogue), ao, io, bool(want_raw),
+                                w_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -117,26 +120,44 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
                      alpha: Optional[torch.Tensor] = None,
                      inv_alpha: Optional[torch.Tensor] = None,
                      out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                     want_raw: bool = True, pad: int = -1):
+                     want_raw: bool = True, pad: int = -1,
+                     w_x3: Optional[torch.Tensor] = None):
     """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d. pad -1 is
     the DecoderBlock's ceil(stride / 2), 0 the padding=False window of the chunked codec."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv_transpose1d(x, w_packed, int(cout), int(stride), bias, alpha,
-                                          inv_alpha, ao, io, bool(want_raw), int(pad))
+                                          inv_alpha, ao, io, bool(want_raw), int(pad), w_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
 RU_FUSED_CHANNELS = (64, 96, 128, 192, 256)
 
+# The bf16x3 split MFMA path (include/vrvq.h, csrc/conv_x3.h) for the stride-1 convs of the
+# inference path; VRVQ_CONV_X3=0 keeps every conv on the fp32-input MFMA (A/B and tests).
+X3 = os.environ.get("VRVQ_CONV_X3", "1") != "0"
+X3_TAPS = (1, 2, 3, 7)
+
+
+def x3_size(cin: int, k: int, cout_pad: int) -> int:
+    ck = 32 if k == 1 else 16 if k <= 3 else 8
+    no = k * ck // 8
+    return -(-cin // ck) * 3 * (no + (no & 1)) * cout_pad * 8
+
+
+def pack_x3_weight(w_packed: torch.Tensor, k: int) -> torch.Tensor:
+    """bf16 planes of a packed conv weight ([Cin][k][cout_pad]; k = 2 for the polyphase
+    ConvTranspose1d) for the x3 path: int16 storage, x3_size(...) elements."""
+    return _ops().pack_x3_weight(w_packed, int(k))
+
 
 def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad: int,
                   out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                  want_raw: bool = True):
+                  want_raw: bool = True, w7_x3: Optional[torch.Tensor] = None):
     """Fused ResidualUnit: x + conv1(snake2(conv7_dil(x_snk))) in one launch (include/vrvq.h,
     vrvq_residual_unit). Returns y, or (y | None, snake_next(y)) when out_snake is given."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().residual_unit(x, x_snk, int(dil), w7, b7, alpha2, inv_alpha2, w1, b1, ao, io,
-                                 bool(want_raw))
+                                 bool(want_raw), w7_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -301,6 +322,11 @@ def _register_fakes():
         cout, cin, k = w.shape
         return f32(w, (cin, k, round_up(cout, 128)))
 
+    @reg("vrvq::pack_x3_weight")
+    def _(w_packed, k):
+        cin, _k, cout_pad = w_packed.shape
+        return torch.empty(x3_size(cin, k, cout_pad), dtype=torch.int16, device=w_packed.device)
+
     @reg("vrvq::pack_convt1d_weight")
     def _(w, stride):
         cin, cout, _k = w.shape
@@ -313,19 +339,20 @@ def _register_fakes():
 
     @reg("vrvq::snake_conv1d")
     def _(x, w_packed, cout, stride, pad, dil, bias, alpha, inv_alpha, residual, epilogue,
-          alpha_out, inv_alpha_out, want_raw):
+          alpha_out, inv_alpha_out, want_raw, w_x3=None):
         B, _c, tin = x.shape
         tout = conv_out_len(tin, w_packed.shape[1], stride, pad, dil)
         return pair(x, (B, cout, tout), alpha_out, want_raw)
 
     @reg("vrvq::snake_conv_transpose1d")
     def _(x, w_packed, cout, stride, bias, alpha, inv_alpha, alpha_out, inv_alpha_out, want_raw,
-          pad=-1):
+          pad=-1, w_x3=None):
         B, _c, tin = x.shape
         return pair(x, (B, cout, convt_out_len(tin, stride, pad)), alpha_out, want_raw)
 
     @reg("vrvq::residual_unit")
-    def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw):
+    def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw,
+          w7_x3=None):
         return pair(x, tuple(x.shape), alpha_out, want_raw)
 
     @reg("vrvq::rvq_cross_prep")
