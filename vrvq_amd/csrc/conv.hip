@@ -24,7 +24,9 @@ namespace {
 using namespace vrvq_conv;
 
 template <int BM, int BN, int WM, int NW, int KS, bool X3>
-__global__ __launch_bounds__(64 * NW) void conv_mfma_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
+void conv_mfma_kernel(ConvArgs a) {
   using TC = TileCfg<BM, BN, WM, NW>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
@@ -251,15 +253,14 @@ static int conv_mt_slow() {
   return v;
 }
 
-// Where the bf16x3 path runs when a pre-split weight is given (VRVQ_CONV_X3_RULE=0: every
-// eligible tile). Measured per layer at B = 32 (profiles/r02zd_x3_layers.txt, fp32 -> x3):
-// 384 k7 128x128 3.32 -> 2.55 ms, ConvT 1536->768 1.27 -> 0.69 ms, ConvT 384->192 2.16 ->
-// 1.64 ms, 768 k7 192x64 1.80 -> 1.70 ms, 512 k1 -25 %; the one loss is the 192x64 k = 1
-// tile (768 k1 + skip 0.34 -> 0.37 ms), which keeps the fp32 path.
+// Where the bf16x3 path runs when a pre-split weight is given: every eligible stride-1 tile
+// (VRVQ_CONV_X3_RULE=1: the rule of the first x3 version, which lost on the 192 x 64 k = 1
+// tile before the single-stage, two-workgroups-per-CU loop). Per layer at B = 32:
+// profiles/r02zd_x3_layers.txt (first version), profiles/r02zg_layer_table.txt (this one).
 static int x3_rule() {
   static const int v = [] {
     const char* e = getenv("VRVQ_CONV_X3_RULE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -290,7 +291,7 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   a.mt_slow = conv_mt_slow();
   if constexpr (NW == 4 && BM <= 192 && (KS == 1 || KS == 2 || KS == 3 || KS == 7)) {
     constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
-    size_t lx = x3_lds_bytes<KS, BM>(XW);
+    size_t lx = x3_lds_bytes<KS, BM, BN>(XW);
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
         x3_tile_ok(BM, BN, KS, a)) {

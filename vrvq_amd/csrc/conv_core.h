@@ -133,39 +133,36 @@ __device__ __forceinline__ void conv_mainloop(
   float4 wreg[WQ];
   float xreg[XROWS][XPR];
 
+  // Loads are branch-free, from clamped addresses; the zeroing of out-of-range values (rows
+  // past cin, window positions outside [0, tin)) happens in store_chunk. A conditional load
+  // compiles to an exec-masked branch, and the wait at its join drains every load in flight:
+  // the W loads of the next chunk were waited for before its x loads were even issued.
+  const int wrows = a.cin * KS;  // rows of the packed weight
   auto load_chunk = [&](int ci0) {
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
-      const int idx = tid + q * NT;
+      const int idx = (WQ4 % NT == 0) ? tid + q * NT : min(tid + q * NT, WQ4 - 1);
       const int rr = idx / (BM / 4);
       const int cc = (idx - rr * (BM / 4)) * 4;
-      const float4* src = reinterpret_cast<const float4*>(a.w + (size_t)(ci0 * KS + rr) * a.m_pad + m0 + cc);
-      if (WQ4 % NT == 0 && cin_full) wreg[q] = *src;
-      else wreg[q] = (idx < WQ4 && ci0 + rr / KS < a.cin) ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = min(ci0 * KS + rr, wrows - 1);
+      wreg[q] = *reinterpret_cast<const float4*>(a.w + (size_t)row * a.m_pad + m0 + cc);
     }
     if (interior) {
 #pragma unroll
       for (int rw = 0; rw < XROWS; ++rw) {
-        const int cl = wave + NW * rw;
+        const int cl = min(wave + NW * rw, CK - 1);
         const float* xr = xb + (size_t)(ci0 + cl) * a.tin + xbase;
 #pragma unroll
-        for (int u = 0; u < XPR; ++u) {
-          const int p = lane + 64 * u;
-          xreg[rw][u] = (cl < CK && p < XW) ? xr[p] : 0.0f;
-        }
+        for (int u = 0; u < XPR; ++u) xreg[rw][u] = xr[min(lane + 64 * u, XW - 1)];
       }
     } else {
 #pragma unroll
       for (int rw = 0; rw < XROWS; ++rw) {
-        const int cl = wave + NW * rw;
-        const int ci = ci0 + cl;
+        const int ci = min(ci0 + min(wave + NW * rw, CK - 1), a.cin - 1);
         const float* xr = xb + (size_t)ci * a.tin;
 #pragma unroll
-        for (int u = 0; u < XPR; ++u) {
-          const int p = lane + 64 * u;
-          const int t = xbase + p;
-          xreg[rw][u] = (cl < CK && ci < a.cin && p < XW && t >= 0 && t < a.tin) ? xr[t] : 0.0f;
-        }
+        for (int u = 0; u < XPR; ++u)
+          xreg[rw][u] = xr[min(max(xbase + lane + 64 * u, 0), a.tin - 1)];
       }
     }
   };
@@ -173,8 +170,14 @@ __device__ __forceinline__ void conv_mainloop(
     float* ws = stg;
     float* xs = stg + KROWS * BM;
 #pragma unroll
-    for (int q = 0; q < WQ; ++q)
-      if (WQ4 % NT == 0 || tid + q * NT < WQ4) reinterpret_cast<float4*>(ws)[tid + q * NT] = wreg[q];
+    for (int q = 0; q < WQ; ++q) {
+      const int idx = tid + q * NT;
+      if (WQ4 % NT == 0 || idx < WQ4) {
+        const int rr = idx / (BM / 4);
+        reinterpret_cast<float4*>(ws)[idx] =
+            (cin_full || ci0 + rr / KS < a.cin) ? wreg[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
 #pragma unroll
     for (int rw = 0; rw < XROWS; ++rw) {
       const int cl = wave + NW * rw;
@@ -185,7 +188,9 @@ __device__ __forceinline__ void conv_mainloop(
 #pragma unroll
       for (int u = 0; u < XPR; ++u) {
         const int p = lane + 64 * u;
-        float v = xreg[rw][u];
+        const int t = xbase + p;
+        const bool ok = ci < a.cin && p < XW && (interior || (t >= 0 && t < a.tin));
+        float v = ok ? xreg[rw][u] : 0.0f;
         if (sn) v = snake_act(v, al, ia);  // snake(0) = 0: zero padding commutes with Snake
         if (a.ssh) {
           if (p < XW) xs[cl * XWP + (p & (a.stride - 1)) * XP + (p >> a.ssh)] = v;
@@ -200,9 +205,13 @@ __device__ __forceinline__ void conv_mainloop(
   load_chunk(0);
   store_chunk(smem, 0);
   __syncthreads();
+  const int last = ((a.cin - 1) / CK) * CK;
   for (int ci0 = 0; ci0 < a.cin; ci0 += CK) {
-    const bool more = ci0 + CK < a.cin;
-    if (more) load_chunk(ci0 + CK);  // global loads in flight during the MFMAs below
+    // next chunk's loads in flight during the MFMAs below; unconditional (the last chunk
+    // reloads itself into the idle stage) so the compiler cannot sink them past the MFMAs
+    const int cn = min(ci0 + CK, last);
+    load_chunk(cn);
+    __builtin_amdgcn_sched_barrier(0);
     const float* ws = smem + cur * STG;
     const float* xs = ws + KROWS * BM;
     // ---- MFMA over the chunk: K order = (tap, channel pair) ----
@@ -245,7 +254,7 @@ __device__ __forceinline__ void conv_mainloop(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (more) store_chunk(smem + (cur ^ 1) * STG, ci0 + CK);
+    store_chunk(smem + (cur ^ 1) * STG, cn);
     __syncthreads();
     cur ^= 1;
   }

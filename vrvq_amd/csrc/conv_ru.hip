@@ -34,7 +34,9 @@ struct RuArgs {
 };
 
 template <int BM, int BN, int WM, int NW, bool X3>
-__global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
+void ru_fused_kernel(RuArgs ra) {
   using TC = TileCfg<BM, BN, WM, NW>;
   constexpr int RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
   constexpr int NS = BM / 2;   // phase-2 MFMA steps (k = 2 channels per step)
@@ -122,15 +124,14 @@ __global__ __launch_bounds__(64 * NW) void ru_fused_kernel(RuArgs ra) {
   conv_epilogue<BM, BN, WM, NW>(ra.p2, smem, acc, b, 0, n0);
 }
 
-// Measured at B = 32 (profiles/r02zd_x3_layers.txt): the x3 phase 1 wins for C = 64
-// (1.17 -> 1.02 ms per unit) and C = 128 (1.95 -> 1.93 ms) and loses for C = 96 / 192
-// (+12 % to +23 %): its LDS stages leave room for one workgroup per CU (the fp32 kernels
-// run two or three), so nothing overlaps the fp32 phase 2 and the epilogue.
-// VRVQ_RU_X3=0: never, 1: C = 64 / 128 (default), 2: every C <= 192.
+// x3 phase 1 for every C <= 192 (C = 256: its 256-row weight stage leaves room for one
+// workgroup per CU; it keeps the fp32 path). Measured at B = 32 with the single-stage x3
+// loop: RU 96 2.12 -> 1.77 ms, RU 192 4.00 -> 3.15 ms, RU 128 1.97 -> 1.35 ms per unit
+// (profiles/r02zg_layer_table.txt). VRVQ_RU_X3=0: never, 1: C = 64 / 128 only, 2: all.
 static bool ru_x3_ok(int C) {
   static const int v = [] {
     const char* e = getenv("VRVQ_RU_X3");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v == 2 ? true : v == 1 ? (C == 64 || C == 128) : false;
 }
@@ -155,7 +156,7 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   const long long nblk = (long long)a.n_nt * batch;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
   if constexpr (BM <= 192) {
-    size_t lx = x3_lds_bytes<7, BM>(XW);
+    size_t lx = x3_lds_bytes<7, BM, BN>(XW);
     if (lx < hsz) lx = hsz;
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && XW <= (BN - 1) + 6 * 9 + 1 && lx <= 160 * 1024 && ru_x3_ok(BM)) {

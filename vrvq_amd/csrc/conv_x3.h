@@ -8,9 +8,8 @@
 //     a_h b_h  +  (a_m b_m + a_h b_l + a_l b_h + a_h b_m + a_m b_h)
 // in fp32 (bf16 x bf16 products are exact in fp32). The dropped terms a_m b_l + a_l b_m +
 // a_l b_l are <= 2^-23 |ab|, the size of one fp32 rounding, so the result carries fp32
-// accuracy (tests compare it with the fp32 path and fp64). The h*h terms and the five
-// correction terms go to two accumulators that are added once at the end. 6 bf16 MFMAs per
-// 16 K (192 cycles) replace 8 fp32 MFMAs (512 cycles): 2.7x the MFMA ceiling.
+// accuracy (tests compare it with the fp32 path and fp64). 6 bf16 MFMAs per 16 K
+// (192 cycles) replace 8 fp32 MFMAs (512 cycles): 2.7x the MFMA ceiling.
 //
 // Operand layouts (32x32x16 bf16: lane l, r = l & 31, h = l >> 5 holds A[row r][k = 8h + e]
 // and B[k = 8h + e][col r], e = 0..7): K is ordered in "octets" of 8 consecutive input
@@ -30,6 +29,16 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 namespace vrvq_conv {
+
+// LDS stages of the x3 K loop. 1 (default): one stage, refilled between two barriers after
+// the chunk's MFMAs; half the LDS and no prefetch registers let two workgroups share a CU,
+// and each one's MFMAs cover the other's loads, barriers and epilogue. 2: double-buffered
+// with the next chunk prefetched into registers during the MFMAs, one workgroup per CU for
+// the larger tiles.
+// Tiles up to 128 x 128 take 1 (two workgroups per CU), the 192-row x 128 tiles 2 (their
+// registers allow one wave per SIMD, so the prefetch has to hide the loads).
+template <int BM, int BN>
+constexpr int x3_stages() { return BM * BN <= 128 * 128 ? 1 : 2; }
 
 template <int KS>
 struct X3Cfg {
@@ -97,6 +106,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
   const int XW = (BN - 1) + (KS - 1) * a.dil + 1;
   const int XWP = x3_xwp(XW);
   const int STG = WB + 3 * NC8 * XWP * 16;  // bytes per stage
+  constexpr int X3_STAGES = x3_stages<BM, BN>();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
@@ -106,13 +116,6 @@ __device__ __forceinline__ void conv_mainloop_x3(
   const int nitems = NC8 * XW;
   char* sbase = reinterpret_cast<char*>(smem);
 
-  f32x16 accl[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) accl[i][j][r] = 0.0f;
 
   constexpr int WQ = X3W<KS, BM, NT>::WQ, WTOT = X3W<KS, BM, NT>::TOTAL;
   u32x4 wr[WQ];
@@ -187,10 +190,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
     // reloads itself into the idle stage): under `if (more)` the compiler sinks the loads past
     // the MFMAs into the store block, their only user.
     const int cn = min(c + 1, nchunks - 1);
-    char* nxt = sbase + (cur ^ 1) * STG;
-    load_w(cn);
-    load_x(cn * CK);
-    __builtin_amdgcn_sched_barrier(0);
+    char* nxt = sbase + (cur ^ (X3_STAGES - 1)) * STG;
+    if constexpr (X3_STAGES == 2) {
+      load_w(cn);
+      load_x(cn * CK);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const u32x4* ws = reinterpret_cast<const u32x4*>(sbase + cur * STG);
     const u32x4* xs = reinterpret_cast<const u32x4*>(sbase + cur * STG + WB);
     auto rd = [&](int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
@@ -212,14 +217,15 @@ __device__ __forceinline__ void conv_mainloop_x3(
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          f32x16 t = accl[i][j];
+          // small terms first, then h h (one accumulator: 64 fewer registers, so two
+          // workgroups fit per CU; the chunk's h h products still enter after its corrections)
+          f32x16 t = acc[i][j];
           t = mfma_bf16(av[1][i], bv[1][j], t);  // m m
           t = mfma_bf16(av[0][i], bv[2][j], t);  // h l
           t = mfma_bf16(av[2][i], bv[0][j], t);  // l h
           t = mfma_bf16(av[0][i], bv[1][j], t);  // h m
           t = mfma_bf16(av[1][i], bv[0][j], t);  // m h
-          accl[i][j] = t;
-          acc[i][j] = mfma_bf16(av[0][i], bv[0][j], acc[i][j]);  // h h
+          acc[i][j] = mfma_bf16(av[0][i], bv[0][j], t);  // h h
         }
     };
     {
@@ -237,21 +243,29 @@ __device__ __forceinline__ void conv_mainloop_x3(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    store_w(nxt);
-    store_x(nxt, cn * CK);
+    if constexpr (X3_STAGES == 1) {
+      // Single stage: the refill is not prefetched (its registers would coexist with the
+      // MFMA operands and spill); the other workgroup on the CU runs its MFMAs meanwhile.
+      __syncthreads();  // every wave done with the stage
+      if (c + 1 < nchunks) {
+        load_w(cn);
+        load_x(cn * CK);
+        store_w(nxt);
+        store_x(nxt, cn * CK);
+      }
+    } else {
+      store_w(nxt);
+      store_x(nxt, cn * CK);
+    }
     __syncthreads();
-    cur ^= 1;
+    cur ^= X3_STAGES - 1;
   }
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = acc[i][j] + accl[i][j];
 }
 
 // LDS bytes the x3 mainloop needs for a window of XW positions.
-template <int KS, int BM>
+template <int KS, int BM, int BN>
 inline size_t x3_lds_bytes(int xw) {
-  return 2 * ((size_t)x3_stage_w_bytes<KS, BM>() + 3 * (size_t)X3Cfg<KS>::NC8 * x3_xwp(xw) * 16);
+  return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM>() + 3 * (size_t)X3Cfg<KS>::NC8 * x3_xwp(xw) * 16);
 }
 
 }  // namespace vrvq_conv
