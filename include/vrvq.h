@@ -112,9 +112,12 @@ int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_p
  * snake2, no raw) followed by vrvq_conv1d(k1, residual = x) — bit-identical where both use the
  * same k7 tile height (C <= 192), else the same sums in another fp32 order. Packed by
  * vrvq_pack_conv1d_weight (same cout_pad). Supported: C in {64, 96, 128, 192, 256}, dil <= 9;
- * other C return VRVQ_ERR_UNSUPPORTED (callers use the two-launch form). */
+ * other C return VRVQ_ERR_UNSUPPORTED (callers use the two-launch form). w7_x3 / w1_x3
+ * (nullable, vrvq_pack_x3_weight of w7_packed / w1_packed): the x3 path for the k7 GEMM and,
+ * where the split hs planes fit in LDS (C = 64 / 96 / 192), the k1 GEMM. */
 int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels, int frames,
-                       int dil, const float* w7_packed, const uint16_t* w7_x3, const float* b7,
+                       int dil, const float* w7_packed, const uint16_t* w7_x3,
+                       const uint16_t* w1_x3, const float* b7,
                        const float* alpha2,
                        const float* inv_alpha2, const float* w1_packed, const float* b1,
                        int cout_pad, float* y, const float* alpha_out,

@@ -40,7 +40,7 @@ def _fake():
         return y if out_snake is None else (y, torch.empty_like(y))
 
     def residual_unit(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad,
-                      out_snake=None, want_raw=True, w7_x3=None):
+                      out_snake=None, want_raw=True, w7_x3=None, w1_x3=None):
         B, C, T = x.shape
         CALLS.append(("RU", C, C, 7, 1, dil, T, B, 2.0 * B * C * T * C * 8, True))
         y = torch.empty(B, C, T)

@@ -27,8 +27,8 @@ SIGNATURES = {
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
     "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
-    "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P,
-                           _P, _P],
+    "vrvq_residual_unit": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P,
+                           _P, _P, _P],
     "vrvq_conv_transpose1d": [_P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "vrvq_conv_transpose1d_pad": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
                                   _P, _P],

@@ -410,7 +410,10 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     if (conv_k7_192() == 2) return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
-  if (KS == 2 && a.up > 0 && conv_t_192() && a.M % 192 == 0) {
+  // (the 192-row k1 / ConvT tiles are fp32-path choices: with the x3 weights the 128-row
+  // tiles, two workgroups per CU, are faster — 638 -> 649 audio-sec/s at B = 32,
+  // profiles/r02zh_tile_ab.txt)
+  if (KS == 2 && a.up > 0 && conv_t_192() && a.w3 == nullptr && a.M % 192 == 0) {
     // polyphase ConvTranspose1d with M = Cout * stride phase rows a multiple of 192
     if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
@@ -423,7 +426,7 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   if constexpr (KS == 1) {
     // k = 1 GEMMs with M a multiple of 192 (the 384 / 768-channel ResidualUnit k1 + skip):
     // 192-row tiles read each x column block 2x / 4x instead of 3x / 6x (tuning knob)
-    if (conv_k1_192() && a.M % 192 == 0 && a.M % 128 == 0) {
+    if (conv_k1_192() && a.w3 == nullptr && a.M % 192 == 0 && a.M % 128 == 0) {
       if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
       return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
     }

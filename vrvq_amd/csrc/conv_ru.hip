@@ -30,8 +30,15 @@ struct RuArgs {
   const float* alpha2; // [C]  Snake between the two convs
   const float* inv_alpha2;
   const float* w1;     // [C][1][m_pad]  packed k=1 weight
+  const u32x4* w1x3;   // pre-split W1 (vrvq_pack_x3_weight, k = 1) or null
   int C;
 };
+
+// Phase 2 on the split bf16 MFMA when its three hs planes (6 B per element) fit in the LDS
+// the kernel already holds: C = 64 / 96 / 192 (C = 128 at BN = 128 would need 96 KiB and
+// drop to one workgroup per CU; it keeps the fp32 phase 2).
+template <int BM, int BN>
+constexpr bool ru_p2x3() { return BM * BN * 6 <= 80 * 1024; }
 
 template <int BM, int BN, int WM, int NW, bool X3>
 __global__ __launch_bounds__(64 * NW)
@@ -63,6 +70,98 @@ void ru_fused_kernel(RuArgs ra) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
+
+  if constexpr (X3 && ru_p2x3<BM, BN>()) {
+    if (ra.w1x3 != nullptr) {
+      // ---- mid: hs = snake2(h + b7) split into three bf16 planes [plane][C/8][BN][8]: the
+      // lane's 4 consecutive rows of each accumulator group are half of one channel octet
+      constexpr int NC8 = BM / 8;
+      char* hsb = reinterpret_cast<char*>(smem);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row0 = wm * TM + i * 32 + 8 * g + 4 * lh;
+          float bb[4], al[4], ia[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = row0 + u < C;
+            bb[u] = ok ? ra.b7[row0 + u] : 0.0f;
+            al[u] = ok ? ra.alpha2[row0 + u] : 0.0f;
+            ia[u] = ok ? ra.inv_alpha2[row0 + u] : 0.0f;
+          }
+          const int c8 = (wm * TM + i * 32 + 8 * g) / 8;
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              v[u] = row0 + u < C ? snake_act(acc[i][j][4 * g + u] + bb[u], al[u], ia[u]) : 0.0f;
+            unsigned h[2], m[2], l[2];
+            split3x2(v[0], v[1], h[0], m[0], l[0]);
+            split3x2(v[2], v[3], h[1], m[1], l[1]);
+            const int col = wn * TN + j * 32 + lr;
+            const size_t off = ((size_t)c8 * BN + col) * 16 + lh * 8;
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u32x2*>(hsb + off) = u32x2{h[0], h[1]};
+            *reinterpret_cast<u32x2*>(hsb + (size_t)NC8 * BN * 16 + off) = u32x2{m[0], m[1]};
+            *reinterpret_cast<u32x2*>(hsb + 2 * (size_t)NC8 * BN * 16 + off) = u32x2{l[0], l[1]};
+          }
+        }
+      __syncthreads();
+      // ---- phase 2: acc = W1 * hs, K = C in steps of 16 channels (octets 2q | 2q + 1 on the
+      // lane halves: the K order of the x3 k = 1 conv, so the fused unit and the two launches
+      // agree bit for bit). W1 planes from L2, one step ahead.
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+      constexpr int NQ = BM / 16;
+      const u32x4* hs = reinterpret_cast<const u32x4*>(hsb);
+      auto lda = [&](int q, u32x4 (&av)[3][RM]) {
+        const int o = 2 * q + lh;  // global octet; k = 1 packing: chunks of 4 octets
+        const int ch = o >> 2, oo = o & 3;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+            av[p][i] = ra.w1x3[((size_t)(ch * 3 + p) * 4 + oo) * a.m_pad + wm * TM + i * 32 + lr];
+      };
+      u32x4 an[3][RM];
+      lda(0, an);
+#pragma unroll 2
+      for (int q = 0; q < NQ; ++q) {
+        u32x4 ac[3][RM], bv[3][RN];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int i = 0; i < RM; ++i) ac[p][i] = an[p][i];
+        lda(min(q + 1, NQ - 1), an);
+        const int o = 2 * q + lh;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) bv[p][j] = hs[((size_t)p * NC8 + o) * BN + wn * TN + j * 32 + lr];
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            f32x16 t = acc[i][j];
+            t = mfma_bf16(ac[1][i], bv[1][j], t);  // m m
+            t = mfma_bf16(ac[0][i], bv[2][j], t);  // h l
+            t = mfma_bf16(ac[2][i], bv[0][j], t);  // l h
+            t = mfma_bf16(ac[0][i], bv[1][j], t);  // h m
+            t = mfma_bf16(ac[1][i], bv[0][j], t);  // m h
+            acc[i][j] = mfma_bf16(ac[0][i], bv[0][j], t);  // h h
+          }
+      }
+      __syncthreads();  // hs reads done: the epilogue reuses the LDS
+      conv_epilogue<BM, BN, WM, NW>(ra.p2, smem, acc, b, 0, n0);
+      return;
+    }
+  }
 
   // ---- mid: hs[row][col] = snake2(h + b7) in the MFMA D layout (rows >= C: zero) ----
   float* hs = smem;
@@ -158,6 +257,7 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   if constexpr (BM <= 192) {
     size_t lx = x3_lds_bytes<7, BM, BN>(XW);
     if (lx < hsz) lx = hsz;
+    if (ru_p2x3<BM, BN>() && ra.w1x3 != nullptr && lx < (size_t)BM * BN * 6) lx = (size_t)BM * BN * 6;
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && XW <= (BN - 1) + 6 * 9 + 1 && lx <= 160 * 1024 && ru_x3_ok(BM)) {
       if (lx > 64 * 1024) {
@@ -185,7 +285,8 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
 
 extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch, int channels,
                                   int frames, int dil, const float* w7_packed,
-                                  const uint16_t* w7_x3, const float* b7,
+                                  const uint16_t* w7_x3, const uint16_t* w1_x3,
+                                  const float* b7,
                                   const float* alpha2, const float* inv_alpha2,
                                   const float* w1_packed, const float* b1, int cout_pad,
                                   float* y, const float* alpha_out, const float* inv_alpha_out,
@@ -208,6 +309,7 @@ extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch,
   q.bias = b1; q.res = x; q.y = y; q.alpha_o = alpha_out; q.inv_alpha_o = inv_alpha_out;
   q.ys = y_snake;
   ra.b7 = b7; ra.alpha2 = alpha2; ra.inv_alpha2 = inv_alpha2; ra.w1 = w1_packed;
+  ra.w1x3 = w7_x3 != nullptr ? reinterpret_cast<const u32x4*>(w1_x3) : nullptr;
   ra.C = channels;
   hipStream_t st = as_stream(stream);
   switch (channels) {

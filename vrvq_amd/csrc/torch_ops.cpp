@@ -260,7 +260,8 @@ std::tuple<Tensor, Tensor> residual_unit(const Tensor& x, const Tensor& x_snk, i
                                          const Tensor& w1, const Tensor& b1,
                                          const optional<Tensor>& alpha_out,
                                          const optional<Tensor>& inv_alpha_out, bool want_raw,
-                                         const optional<Tensor>& w7_x3) {
+                                         const optional<Tensor>& w7_x3,
+                                         const optional<Tensor>& w1_x3) {
   check_t(x, "x");
   check_on(x_snk, x, "x_snk");
   check_on(w7, x, "w7");
@@ -279,7 +280,8 @@ std::tuple<Tensor, Tensor> residual_unit(const Tensor& x, const Tensor& x_snk, i
   auto [y, ys, _u] = out_pair(x, {B, C, T}, alpha_out, inv_alpha_out, want_raw);
   check_rc(vrvq_residual_unit(x.data_ptr<float>(), x_snk.data_ptr<float>(), (int)B, (int)C,
                               (int)T, (int)dil, w7.data_ptr<float>(),
-                              x3_ptr(w7_x3, x, C, 7, w7.size(2)), b7.data_ptr<float>(),
+                              x3_ptr(w7_x3, x, C, 7, w7.size(2)),
+                              x3_ptr(w1_x3, x, C, 1, w1.size(2)), b7.data_ptr<float>(),
                               alpha2.data_ptr<float>(), inv_alpha2.data_ptr<float>(),
                               w1.data_ptr<float>(), b1.data_ptr<float>(), (int)w7.size(2),
                               opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
@@ -870,7 +872,7 @@ TORCH_LIBRARY(vrvq, m) {
   m.def(
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw, Tensor? w7_x3=None) -> (Tensor, Tensor)");
+      "bool want_raw, Tensor? w7_x3=None, Tensor? w1_x3=None) -> (Tensor, Tensor)");
   m.def("rvq_cross_prep(Tensor w_in_t, Tensor w_out, Tensor b_out) -> (Tensor, Tensor)");
   m.def("rvq_frag(Tensor cbn) -> Tensor");
   m.def(

@@ -210,7 +210,8 @@ class ResidualUnit(nn.Module):
                                      self.block[1].bias.detach(), a2, ia2, w1,
                                      self.block[3].bias.detach(), cp7,
                                      out_snake=out_snake.prepared(), want_raw=want_raw,
-                                     w7_x3=self.block[1].prepared_x3())
+                                     w7_x3=self.block[1].prepared_x3(),
+                                     w1_x3=self.block[3].prepared_x3())
         return self.run_two_launch(x, x_snk, out_snake, want_raw)
 
     def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool):

@@ -152,12 +152,13 @@ def pack_x3_weight(w_packed: torch.Tensor, k: int) -> torch.Tensor:
 
 def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad: int,
                   out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                  want_raw: bool = True, w7_x3: Optional[torch.Tensor] = None):
+                  want_raw: bool = True, w7_x3: Optional[torch.Tensor] = None,
+                  w1_x3: Optional[torch.Tensor] = None):
     """Fused ResidualUnit: x + conv1(snake2(conv7_dil(x_snk))) in one launch (include/vrvq.h,
     vrvq_residual_unit). Returns y, or (y | None, snake_next(y)) when out_snake is given."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().residual_unit(x, x_snk, int(dil), w7, b7, alpha2, inv_alpha2, w1, b1, ao, io,
-                                 bool(want_raw), w7_x3)
+                                 bool(want_raw), w7_x3, w1_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -352,7 +353,7 @@ def _register_fakes():
 
     @reg("vrvq::residual_unit")
     def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw,
-          w7_x3=None):
+          w7_x3=None, w1_x3=None):
         return pair(x, tuple(x.shape), alpha_out, want_raw)
 
     @reg("vrvq::rvq_cross_prep")
