@@ -16,7 +16,9 @@ bpf / kbps are job-wide. Rank 0 prints one JSON line, including
                 against HBM, bytes per SURVEY.md §8(d), per-launch durations from HIP events
                 recorded on the launch stream inside the timed steps; per-kernel split from the
                 committed rocprofv3 summary; traffic from the committed PMC passes;
-  roofline_conv the fp32-MFMA conv stacks against the fp32 matrix peak;
+  roofline_conv the conv stacks (fp32 arithmetic: the x3 split-bf16 MFMA path for stride-1
+                convs, fp32-input MFMA for the strided ones) against the fp32 matrix peak
+                and against the x3 ceiling;
   cpu_baseline  oracle/torch_ref.py (a pure-PyTorch CPU restatement of the reference forward,
                 fixture-pinned) timed on this host on a bounded sample (rank 0, N=1 only).
 """
@@ -39,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (= vector peak)
+X3_PEAK_TFLOPS = 2516.6 / 6    # fp32 FLOPs on the bf16 MFMA with the exact 3-way split (6 products)
 CLIP_SAMPLES = 44100
 SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
@@ -391,7 +394,14 @@ def main():
                               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
                               "flops_per_step": flops,
-                              "note": "algorithmic conv FLOPs / (step time - RVQ launches)"},
+                              "x3_peak": X3_PEAK_TFLOPS,
+                              "frac_x3": round(conv_tflops / X3_PEAK_TFLOPS, 4),
+                              "note": "algorithmic fp32 conv FLOPs / (step time - RVQ launches). "
+                                      "Stride-1 convs run the x3 path (csrc/conv_x3.h): both "
+                                      "operands split exactly into 3 bf16 terms, 6 bf16 MFMAs "
+                                      "per fp32 product pair, fp32 accumulate (fp32-accurate; "
+                                      "its ceiling x3_peak = bf16 dense peak / 6); peak = the "
+                                      "fp32-input MFMA peak the strided convs run on"},
         }
         if levels_rep is not None:
             res["levels"] = levels_rep

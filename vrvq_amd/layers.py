@@ -202,7 +202,11 @@ class ResidualUnit(nn.Module):
         LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
         k1 conv adds the skip. Either way the output is (y if want_raw, out_snake(y)) (bit for
         bit the same for C <= 192, include/vrvq.h)."""
-        if self.fused and x.shape[1] in ops.RU_FUSED_CHANNELS:
+        C = x.shape[1]
+        # C = 256 with the x3 weights: the two launches (k7 on the x3 path at 128-row tiles,
+        # then k1 + skip) beat the fused kernel, whose 256-row x3 weight stage does not fit
+        # twice per CU and therefore keeps the fp32 MFMA (profiles/r02zi_bench_ab.txt)
+        if self.fused and C in ops.RU_FUSED_CHANNELS and not (C == 256 and ops.X3 and ops.RU256_SPLIT):
             w7, cp7 = self.block[1].prepared()
             w1, cp1 = self.block[3].prepared()
             a2, ia2 = self.block[2].prepared()

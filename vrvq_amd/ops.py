@@ -136,6 +136,7 @@ RU_FUSED_CHANNELS = (64, 96, 128, 192, 256)
 # inference path; VRVQ_CONV_X3=0 keeps every conv on the fp32-input MFMA (A/B and tests).
 X3 = os.environ.get("VRVQ_CONV_X3", "1") != "0"
 X3_TAPS = (1, 2, 3, 7)
+RU256_SPLIT = os.environ.get("VRVQ_RU256_SPLIT", "1") != "0"
 
 
 def x3_size(cin: int, k: int, cout_pad: int) -> int:
