@@ -107,22 +107,27 @@ def main():
         m(torch.zeros(args.batch, 1, 44100), 44100, None, 1.0)
     rows = list(csv.DictReader(open(args.trace)))
     conv = [r for r in rows if any(k in r["Kernel_Name"] for k in
-                                   ("conv_mfma_kernel", "conv_small", "ru_fused_kernel"))]
+                                   ("conv_mfma_kernel", "conv_small", "conv_cout1", "ru_fused_kernel"))]
     step = conv[-len(CALLS):]
     tot_t = tot_f = 0.0
-    print(f"{'layer':42s} {'kernel':22s} {'us':>9s} {'GFLOP':>8s} {'TF/s':>7s} {'%pk':>5s}")
+    # %pk against the ceiling of the path the kernel runs: the x3 split-bf16 MFMA (template
+    # flag true: bf16 dense peak / 6 = 419.4 TF/s of fp32 work) or the fp32-input MFMA (157.3)
+    print(f"{'layer':42s} {'kernel':34s} {'us':>9s} {'GFLOP':>8s} {'TF/s':>7s} {'%pk':>5s}")
     for c, r in zip(CALLS, step):
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         kn = r["Kernel_Name"]
         i = kn.find("<")
-        pre = "mfma" if "mfma" in kn else ("ru" if "ru_fused" in kn else "small")
-        kn = pre + kn[i:kn.find(">") + 1]
+        pre = ("mfma" if "mfma" in kn else "ru" if "ru_fused" in kn else
+               "cout1" if "cout1" in kn else "small")
+        x3 = kn[i:kn.find(">") + 1].endswith("true>")
+        kn = pre + kn[i:kn.find(">") + 1] if i >= 0 else pre
         tf = c[8] / (us * 1e-6) / 1e12
         tot_t += us
         tot_f += c[8]
         desc = (f"RU {c[1]} k7+k1 d{c[5]} T{c[6]} (fused)" if c[0] == "RU" else
                 f"{c[0]} {c[1]}->{c[2]} k{c[3]} s{c[4]} d{c[5]} T{c[6]}{' +res' if c[9] else ''}")
-        print(f"{desc:42s} {kn:22s} {us:9.1f} {c[8]/1e9:8.1f} {tf:7.1f} {tf/157.3*100:5.1f}")
+        pk = 419.4 if x3 else 157.3
+        print(f"{desc:42s} {kn:34s} {us:9.1f} {c[8]/1e9:8.1f} {tf:7.1f} {tf/pk*100:5.1f}")
     print(f"total conv: {tot_t/1e3:.2f} ms, {tot_f/1e12:.3f} TFLOP, {tot_f/(tot_t*1e-6)/1e12:.1f} TF/s")
 
 

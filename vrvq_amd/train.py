@@ -24,11 +24,22 @@ reference's order, so a seeded step draws bit-identical values.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from . import ops
+
+# Forward and adjoint convs of the training step on the bf16x3 split MFMA path (csrc/conv_x3.h:
+# fp32-accurate; the weights change every step, so their split planes are packed per call).
+# VRVQ_TRAIN_X3=0 keeps them on the fp32-input MFMA (A/B).
+TRAIN_X3 = ops.X3 and os.environ.get("VRVQ_TRAIN_X3", "1") != "0"
+
+
+def _x3(wp: torch.Tensor, k: int) -> Optional[torch.Tensor]:
+    """Split planes of a packed weight for a stride-1 conv (k taps) or a polyphase ConvT (k=2)."""
+    return ops.pack_x3_weight(wp, k) if TRAIN_X3 and k in ops.X3_TAPS else None
 
 
 def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -51,10 +62,11 @@ class _SnakeConv(torch.autograd.Function):
             wp, cp = ops.pack_conv1d_weight(w)
             y = ops.conv1d(x, wp, cout, cp, k, stride, pad, dil, bias=b, alpha=a, inv_alpha=inv,
                            residual=_c(residual.detach()) if residual is not None else None,
-                           epilogue=epi)
+                           epilogue=epi, w_x3=_x3(wp, k) if stride == 1 else None)
         else:
             wp, cp = ops.pack_convt1d_weight(w, stride)
-            y = ops.conv_transpose1d(x, wp, cout, cp, stride, bias=b, alpha=a, inv_alpha=inv)
+            y = ops.conv_transpose1d(x, wp, cout, cp, stride, bias=b, alpha=a, inv_alpha=inv,
+                                     w_x3=_x3(wp, 2))
         ctx.spec = spec
         ctx.has_alpha = alpha is not None
         ctx.has_res = residual is not None
@@ -84,10 +96,10 @@ class _SnakeConv(torch.autograd.Function):
             cin = x.shape[1]
             if kind == "conv" and stride == 1:
                 wf, cpf = ops.pack_conv1d_flip(w)
-                dxs = ops.conv1d(gy, wf, cin, cpf, k, 1, dil * (k - 1) - pad, dil)
+                dxs = ops.conv1d(gy, wf, cin, cpf, k, 1, dil * (k - 1) - pad, dil, w_x3=_x3(wf, k))
             elif kind == "conv":  # strided conv: adjoint is the polyphase ConvTranspose1d
                 wt, cpt = ops.pack_convt1d_weight(w, stride)
-                dxs = ops.conv_transpose1d(gy, wt, cin, cpt, stride)
+                dxs = ops.conv_transpose1d(gy, wt, cin, cpt, stride, w_x3=_x3(wt, 2))
             else:  # ConvTranspose1d: adjoint is the strided conv with the same weight array
                 wc, cpc = ops.pack_conv1d_weight(w)
                 dxs = ops.conv1d(gy, wc, cin, cpc, k, stride, pad, 1)
