@@ -95,7 +95,11 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
  * w_x3 = vrvq_pack_x3_weight(w_packed) (null: the fp32-input MFMA path) the stride-1 convs
  * (k in {1, 2, 3, 7}; also the ConvTranspose1d and the ResidualUnit's k7) split both operands
  * exactly into three bf16 terms and accumulate the six products >= 2^-16 of each fp32
- * product in fp32 — fp32 accuracy at 2.7x the MFMA ceiling. Strided convs ignore w_x3.
+ * product in fp32 — fp32 accuracy at 2.7x the MFMA ceiling. A strided conv (k = 2 stride,
+ * stride a power of two: the EncoderBlock downsamplers, models/layers.py:83-88) given w_x3 runs
+ * as a stride-1 2-tap conv over the phase-split view xv[c*s + r][m] = x[c][m*s + r - pad]:
+ * w_x3 then holds vrvq_pack_x3_weight(cin * stride, k = 2) of the packed phase-split weight
+ * W'[co][c*s + r][j] = W[co][c][j*s + r] (other strided shapes: VRVQ_ERR_UNSUPPORTED).
  * vrvq_x3_weight_size gives the buffer length in uint16 elements. */
 int vrvq_x3_weight_size(int cin, int k, int cout_pad, long long* n_u16);
 int vrvq_pack_x3_weight(const float* w_packed, int cin, int k, int cout_pad, uint16_t* w_x3,

@@ -276,6 +276,40 @@ def test_conv1d_x3_vs_torch(case):
     assert e3 <= 4 * e32 + 2e-7, (e3, e32)
 
 
+@pytest.mark.parametrize("case", [(2, 64, 128, 1000, 2, 1, True), (2, 128, 256, 401, 4, 2, True),
+                                  (2, 256, 512, 100, 8, 4, False), (2, 512, 1024, 696, 8, 4, False),
+                                  (1, 64, 128, 513, 2, 0, True), (1, 8, 16, 37, 4, 2, True),
+                                  (3, 24, 40, 77, 2, 1, False), (1, 16, 32, 31, 8, 0, True)])
+def test_conv1d_strided_x3_vs_torch(case):
+    """Strided convs (k = 2s) on the x3 loop through the phase-split view of x (vrvq_conv1d with
+    w_x3 for stride > 1) against torch fp64, within a small multiple of the fp32 path's error."""
+    B, cin, cout, T, s, p, use_snake = case
+    gen = torch.Generator(device="cpu").manual_seed(s * 7919 + T + cin)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cout, cin, 2 * s, generator=gen) / np.sqrt(cin * 2 * s)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    xin = _snake_ref(x, alpha) if use_snake else x
+    ref = F.conv1d(xin.double(), w.double(), b.double(), stride=s, padding=p).cpu().numpy()
+    wp, cout_pad = ops.pack_conv1d_weight(w)
+    kw = dict(bias=b, alpha=alpha if use_snake else None,
+              inv_alpha=ops.snake_inv_alpha(alpha) if use_snake else None)
+    y32 = ops.conv1d(x, wp, cout, cout_pad, 2 * s, s, p, 1, **kw)
+    y3 = ops.conv1d(x, wp, cout, cout_pad, 2 * s, s, p, 1,
+                    w_x3=ops.pack_x3_strided_weight(w, s), **kw)
+    assert y3.shape == ref.shape
+    e32 = rel_err(y32.cpu().numpy(), ref)
+    e3 = rel_err(y3.cpu().numpy(), ref)
+    assert e3 < 1e-5
+    assert e3 <= 4 * e32 + 2e-7, (e3, e32)
+    a_next = (torch.rand(cout, generator=gen) * 1.5 + 0.5).to(DEV)
+    y4, ys = ops.conv1d(x, wp, cout, cout_pad, 2 * s, s, p, 1,
+                        w_x3=ops.pack_x3_strided_weight(w, s),
+                        out_snake=(a_next, ops.snake_inv_alpha(a_next)), **kw)
+    assert torch.equal(y4, y3)
+    assert rel_err(ys.cpu().numpy(), _snake_ref(y3, a_next).cpu().numpy()) < 1e-6
+
+
 @pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8),
                                   (2, 384, 192, 333, 4), (2, 192, 96, 1000, 2),
                                   (1, 16, 8, 1, 2), (2, 64, 40, 77, 3)])

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--no-snake-out", action="store_true", help="no producer-side Snake output")
     ap.add_argument("--raw", action="store_true",
                     help="also write the raw output next to the Snake one (encoder blocks)")
+    ap.add_argument("--x3", action="store_true", help="the bf16x3 split path (csrc/conv_x3.h)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
@@ -49,15 +50,18 @@ def main():
         b = torch.zeros(C, device=dev)
         x_snk = x.clone()  # snake1(x) in the model; any values time the same
         osn = (ao[:C].contiguous(), ops.snake_inv_alpha(ao[:C].contiguous()))
+        w73 = ops.pack_x3_weight(wp7, 7) if args.x3 else None
+        w13 = ops.pack_x3_weight(wp1, 1) if args.x3 else None
         fn = lambda: ops.residual_unit(x, x_snk, args.dil, wp7, b, alpha, inv, wp1, b, cp,
-                                       out_snake=osn, want_raw=True)
+                                       out_snake=osn, want_raw=True, w7_x3=w73, w1_x3=w13)
         flops = 2.0 * args.batch * C * C * 8 * args.t
     elif args.convt:
         w = (torch.randn(args.cin, args.cout, 2 * args.convt, generator=g) * 0.02).to(dev)
         wp, cp = ops.pack_convt1d_weight(w, args.convt)
         b = torch.zeros(args.cout, device=dev)
+        w3 = ops.pack_x3_weight(wp, 2) if args.x3 else None
         fn = lambda: ops.conv_transpose1d(x, wp, args.cout, cp, args.convt, b, a_in, i_in,
-                                          out_snake=osn, want_raw=True)
+                                          out_snake=osn, want_raw=True, w_x3=w3)
         flops = 2.0 * args.batch * args.cin * args.cout * 2 * args.convt * args.t
     else:
         w = (torch.randn(args.cout, args.cin, args.k, generator=g) * 0.02).to(dev)
@@ -66,8 +70,13 @@ def main():
         pad = (args.k - 1) * args.dil // 2 if args.stride == 1 else (args.stride + 1) // 2
         tout = (args.t + 2 * pad - args.dil * (args.k - 1) - 1) // args.stride + 1
         res = torch.randn(args.batch, args.cout, tout, device=dev) if args.res else None
+        w3 = None
+        if args.x3:
+            w3 = (ops.pack_x3_weight(wp, args.k) if args.stride == 1 else
+                  ops.pack_x3_strided_weight(w, args.stride))
         fn = lambda: ops.conv1d(x, wp, args.cout, cp, args.k, args.stride, pad, args.dil, b, a_in,
-                                i_in, res, out_snake=osn, want_raw=args.raw or args.res or osn is None)
+                                i_in, res, out_snake=osn, want_raw=args.raw or args.res or osn is None,
+                                w_x3=w3)
         flops = 2.0 * args.batch * args.cin * args.cout * args.k * tout
     for _ in range(3):
         fn()

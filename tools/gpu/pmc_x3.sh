@@ -1,0 +1,32 @@
+#!/bin/bash
+# SQ counters of the x3 conv kernels (the largest layers of the config-2 step, B=32), one
+# rocprofv3 --pmc pass per counter set (kernel-trace only), plus HIP-event time per layer.
+cd "$GRAFT_REPO_ROOT" || exit 2
+OUT=gpurun_out/pmc_x3
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() { local name=$1 to=$2; shift 2
+  echo "=== $name"; timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
+  echo "=== $name rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | grep -v "^[WE]20" | tail -1
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; return 0; }
+L1="--x3 --ru --cin 192 --t 22272 --dil 3"
+L2="--x3 --cin 384 --cout 384 --t 5568 --k 7 --dil 3"
+L3="--x3 --ru --cin 96 --t 44544 --dil 3"
+L4="--x3 --ru --cin 128 --t 22272 --dil 3"
+L5="--x3 --cin 768 --cout 768 --t 696 --k 7 --dil 3"
+L6="--x3 --cin 384 --cout 384 --t 5568 --k 1 --res"
+L7="--x3 --cin 256 --cout 512 --t 5568 --k 16 --stride 8"
+L8="--x3 --cin 384 --cout 192 --t 5568 --convt 4"
+P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+P2="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"
+i=0
+for L in "$L1" "$L2" "$L3" "$L4" "$L5" "$L6" "$L7" "$L8"; do
+  i=$((i+1))
+  run l${i}_time 60 python tools/conv_bench.py $L
+  j=0
+  for P in "$P1" "$P2"; do
+    j=$((j+1))
+    run l${i}p${j} 90 rocprofv3 --pmc $P --kernel-include-regex "conv_|ru_" -d $OUT/l${i}p${j} -o run --output-format csv -- python tools/conv_bench.py $L --iters 3
+  done
+done
+exit 0

@@ -305,6 +305,7 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
       return vrvq_launch_status();
     }
   }
+  if (a.psh) return VRVQ_ERR_UNSUPPORTED;  // the phase-split view exists on the x3 loop only
   if (XW > 64 * WinCfg<KS, BN>::PER_ROW) return VRVQ_ERR_UNSUPPORTED;  // window > staged lanes
   size_t lds = 2 * (size_t)(CK * KS * BM + CK * XWP) * sizeof(float);
   if (lds < epi) lds = epi;  // epilogue tile
@@ -365,6 +366,17 @@ static int conv_t_192() {  // tuning override: VRVQ_CONVT_192=0 | 1 (192-row Con
   return v;
 }
 
+// T = 87 layers: the 96-wide tile (one per clip) when it gives at least this many workgroups,
+// else three 32-wide tiles (tuning override VRVQ_CONV_BN96_MIN; each N tile re-streams its M
+// tile's whole weight block, so the narrow tiles triple the weight traffic)
+static long long conv_bn96_min() {
+  static const long long v = [] {
+    const char* e = getenv("VRVQ_CONV_BN96_MIN");
+    return e ? atoll(e) : 384LL;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -375,7 +387,7 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     // T = 87 / 88 layers: one 96-wide tile per clip when that still gives >= 1.5 workgroups
     // per CU, otherwise three 32-wide tiles (more workgroups for the deep-K, narrow-N GEMMs).
     const long long blocks96 = (long long)((a.M + 127) / 128) * batch;
-    bn = blocks96 >= 384 ? 96 : 32;
+    bn = blocks96 >= conv_bn96_min() ? 96 : 32;
   }
   // k = 16 (the stride-8 encoder convs): the 8 MB weight block does not fit in L2, so the
   // 128-wide tile's halved weight re-streaming beats its padding (1490 -> 1323 us at T = 696,
@@ -582,6 +594,15 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
     while ((1 << a.ssh) < stride) ++a.ssh;
   a.ylen = tout; a.epi = epilogue;
   a.w3 = reinterpret_cast<const unsigned*>(w_x3);
+  if (w_x3 != nullptr && stride > 1) {
+    // strided conv on the x3 loop: a stride-1 k = 2 conv over the phase-split view of x
+    // (conv_core.h ConvArgs::psh); w_x3 holds the planes of W'[co][c*s + r][j] = W[co][c][j*s + r]
+    if (k != 2 * stride || a.ssh == 0 || pad >= stride) return VRVQ_ERR_UNSUPPORTED;
+    a.psh = a.ssh; a.ppad = pad; a.pcin = cin; a.ptin = tin;
+    a.cin = cin * stride; a.tin = tout + 1;
+    a.stride = 1; a.pad = 0; a.dil = 1; a.ssh = 0;
+    return dispatch_ks(2, a, batch, as_stream(stream));
+  }
   if (cout <= SMALL_COUT && stride == 1 && cin * k * (cout == 1 ? 1 : SMALL_COUT) <= SMALL_WMAX)
     return launch_small(a, batch, k, as_stream(stream));
   return dispatch_ks(k, a, batch, as_stream(stream));

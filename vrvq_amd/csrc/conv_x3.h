@@ -111,7 +111,11 @@ __device__ __forceinline__ void conv_mainloop_x3(
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
   const u32x4* w3 = reinterpret_cast<const u32x4*>(a.w3);
-  const float* xb = a.x + (size_t)b * a.cin * a.tin;
+  // phase-split view (strided convs, a.psh > 0): view channel cv = c*s + r, position m reads
+  // x[c][m*s + r - ppad]; with psh = 0 the same expressions reduce to x[cv][m]
+  const int psh = a.psh, pmask = (1 << psh) - 1, ppad = a.ppad;
+  const int ptin = psh ? a.ptin : a.tin;
+  const float* xb = a.x + (size_t)b * (psh ? (size_t)a.pcin * a.ptin : (size_t)a.cin * a.tin);
   const int xbase = n0 - a.pad;
   const int nitems = NC8 * XW;
   char* sbase = reinterpret_cast<char*>(smem);
@@ -146,7 +150,11 @@ __device__ __forceinline__ void conv_mainloop_x3(
       const int tc = min(max(xbase + pos, 0), a.tin - 1);
       const int cb = ci0 + (e < nitems ? c8 : 0) * 8;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) xr[it][u] = xb[(size_t)min(cb + u, a.cin - 1) * a.tin + tc];
+      for (int u = 0; u < 8; ++u) {
+        const int cv = min(cb + u, a.cin - 1);
+        const int tp = min(max((tc << psh) + (cv & pmask) - ppad, 0), ptin - 1);
+        xr[it][u] = xb[(size_t)(cv >> psh) * ptin + tp];
+      }
     }
   };
   auto store_x = [&](char* stg, int ci0) {
@@ -160,11 +168,15 @@ __device__ __forceinline__ void conv_mainloop_x3(
       const bool okp = t >= 0 && t < a.tin;
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (okp && ci0 + c8 * 8 + u < a.cin) ? xr[it][u] : 0.0f;
+      for (int u = 0; u < 8; ++u) {
+        const int cv = ci0 + c8 * 8 + u;
+        const int tp = (t << psh) + (cv & pmask) - ppad;  // = t without the view
+        v[u] = (okp && cv < a.cin && tp >= 0 && tp < ptin) ? xr[it][u] : 0.0f;
+      }
       if (a.alpha != nullptr) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int ci = min(ci0 + c8 * 8 + u, a.cin - 1);
+          const int ci = min(ci0 + c8 * 8 + u, a.cin - 1) >> psh;
           v[u] = snake_act(v[u], a.alpha[ci], a.inv_alpha[ci]);  // snake(0) = 0
         }
       }

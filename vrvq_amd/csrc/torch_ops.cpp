@@ -210,7 +210,10 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
     TORCH_CHECK(residual->sizes() == at::IntArrayRef({B, cout, tout}),
                 "conv1d: residual shape must equal the output shape");
   auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
-  const uint16_t* w3 = x3_ptr(w_x3, x, cin, k, cout_pad);
+  // strided conv (k = 2 stride): w_x3 holds the planes of the phase-split weight (Cin * stride
+  // view channels, 2 taps; include/vrvq.h vrvq_conv1d)
+  const uint16_t* w3 = stride > 1 ? x3_ptr(w_x3, x, cin * stride, 2, cout_pad)
+                                  : x3_ptr(w_x3, x, cin, k, cout_pad);
   check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha), fp(inv_alpha),
                        w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad, (int)k, (int)stride,
                        (int)pad, (int)dil, fp(bias), fp(residual), (int)epilogue, opt_ptr(y),

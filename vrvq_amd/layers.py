@@ -89,15 +89,23 @@ class WNConv1d(nn.Module):
         return self._cache[1], self._cache[2]
 
     def prepared_x3(self):
-        """bf16 planes of the packed weight for the x3 MFMA path (stride-1 k in {1, 3, 7} with
-        >= 8 input channels), or None (fp32-input MFMA path)."""
-        k = self.kernel_size[0]
-        if not (ops.X3 and self.stride[0] == 1 and k in ops.X3_TAPS and self.in_channels >= 8):
+        """bf16 planes of the packed weight for the x3 MFMA path, or None (fp32-input MFMA
+        path): stride-1 k in {1, 3, 7} with >= 8 input channels, and the strided encoder convs
+        (k = 2s, s a power of two) as a stride-1 k = 2 conv over the phase-split view of x,
+        whose weight is W'[co][c*s + r][j] = W[co][c][j*s + r] (include/vrvq.h vrvq_conv1d)."""
+        k, s = self.kernel_size[0], self.stride[0]
+        if not ops.X3 or self.in_channels < 8:
             return None
-        wp, _ = self.prepared()
+        strided = (s > 1 and k == 2 * s and s & (s - 1) == 0 and ops.X3_STRIDED)
+        if not ((s == 1 and k in ops.X3_TAPS) or strided):
+            return None
         key = _param_key(self.weight_g, self.weight_v)
         if self._cache_x3 is None or self._cache_x3[0] != key:
-            self._cache_x3 = (key, ops.pack_x3_weight(wp, k))
+            if strided:
+                self._cache_x3 = (key, ops.pack_x3_strided_weight(self.folded_weight(), s))
+            else:
+                wp, _ = self.prepared()
+                self._cache_x3 = (key, ops.pack_x3_weight(wp, k))
         return self._cache_x3[1]
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,

@@ -137,6 +137,9 @@ RU_FUSED_CHANNELS = (64, 96, 128, 192, 256)
 X3 = os.environ.get("VRVQ_CONV_X3", "1") != "0"
 X3_TAPS = (1, 2, 3, 7)
 RU256_SPLIT = os.environ.get("VRVQ_RU256_SPLIT", "1") != "0"
+# The strided encoder convs (k = 2s) on the x3 path through the phase-split view (vrvq_conv1d);
+# VRVQ_CONV_X3_STRIDED=0 keeps them on the fp32-input MFMA's strided window (A/B).
+X3_STRIDED = os.environ.get("VRVQ_CONV_X3_STRIDED", "1") != "0"
 
 
 def x3_size(cin: int, k: int, cout_pad: int) -> int:
@@ -149,6 +152,19 @@ def pack_x3_weight(w_packed: torch.Tensor, k: int) -> torch.Tensor:
     """bf16 planes of a packed conv weight ([Cin][k][cout_pad]; k = 2 for the polyphase
     ConvTranspose1d) for the x3 path: int16 storage, x3_size(...) elements."""
     return _ops().pack_x3_weight(w_packed, int(k))
+
+
+def pack_x3_strided_weight(w: torch.Tensor, stride: int) -> torch.Tensor:
+    """x3 planes for a strided conv (w: (Cout, Cin, 2*stride), stride a power of two): the
+    planes of W'[co][c*s + r][j] = W[co][c][j*s + r], the 2-tap weight of the stride-1 conv over
+    the phase-split view of x that vrvq_conv1d runs when given w_x3 for stride > 1."""
+    co, ci, k = w.shape
+    s = int(stride)
+    if k != 2 * s or s < 2 or s & (s - 1):
+        raise RuntimeError("pack_x3_strided_weight: kernel must be 2*stride, stride a power of 2")
+    wv = w.reshape(co, ci, 2, s).permute(0, 1, 3, 2).reshape(co, ci * s, 2).contiguous()
+    wp, _ = pack_conv1d_weight(wv)
+    return pack_x3_weight(wp, 2)
 
 
 def residual_unit(x, x_snk, dil: int, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad: int,

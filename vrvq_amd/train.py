@@ -42,6 +42,12 @@ def _x3(wp: torch.Tensor, k: int) -> Optional[torch.Tensor]:
     return ops.pack_x3_weight(wp, k) if TRAIN_X3 and k in ops.X3_TAPS else None
 
 
+def _x3s(w: torch.Tensor, k: int, stride: int) -> Optional[torch.Tensor]:
+    """Split planes of a strided conv's phase-split weight (k = 2s, s a power of two)."""
+    ok = TRAIN_X3 and ops.X3_STRIDED and k == 2 * stride and stride & (stride - 1) == 0
+    return ops.pack_x3_strided_weight(w, stride) if ok and w.shape[1] >= 8 else None
+
+
 def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None else t.contiguous()
 
@@ -62,7 +68,7 @@ class _SnakeConv(torch.autograd.Function):
             wp, cp = ops.pack_conv1d_weight(w)
             y = ops.conv1d(x, wp, cout, cp, k, stride, pad, dil, bias=b, alpha=a, inv_alpha=inv,
                            residual=_c(residual.detach()) if residual is not None else None,
-                           epilogue=epi, w_x3=_x3(wp, k) if stride == 1 else None)
+                           epilogue=epi, w_x3=_x3(wp, k) if stride == 1 else _x3s(w, k, stride))
         else:
             wp, cp = ops.pack_convt1d_weight(w, stride)
             y = ops.conv_transpose1d(x, wp, cout, cp, stride, bias=b, alpha=a, inv_alpha=inv,
@@ -102,7 +108,7 @@ class _SnakeConv(torch.autograd.Function):
                 dxs = ops.conv_transpose1d(gy, wt, cin, cpt, stride, w_x3=_x3(wt, 2))
             else:  # ConvTranspose1d: adjoint is the strided conv with the same weight array
                 wc, cpc = ops.pack_conv1d_weight(w)
-                dxs = ops.conv1d(gy, wc, cin, cpc, k, stride, pad, 1)
+                dxs = ops.conv1d(gy, wc, cin, cpc, k, stride, pad, 1, w_x3=_x3s(w, k, stride))
             if dxs.shape != x.shape:
                 raise RuntimeError(f"adjoint conv shape {tuple(dxs.shape)} != {tuple(x.shape)}")
             if ctx.has_alpha:
