@@ -119,7 +119,10 @@ def main():
         i = kn.find("<")
         pre = ("mfma" if "mfma" in kn else "ru" if "ru_fused" in kn else
                "cout1" if "cout1" in kn else "small")
-        x3 = kn[i:kn.find(">") + 1].endswith("true>")
+        targs = [t.strip() for t in kn[i + 1:kn.find(">")].split(",")] if i >= 0 else []
+        # conv_mfma_kernel<BM, BN, WM, NW, KS, X3[, PH]>, ru_fused_kernel<C, BN, WM, NW, X3>
+        x3 = ((pre == "mfma" and len(targs) >= 6 and targs[5] == "true") or
+              (pre == "ru" and len(targs) >= 5 and targs[4] == "true"))
         kn = pre + kn[i:kn.find(">") + 1] if i >= 0 else pre
         tf = c[8] / (us * 1e-6) / 1e12
         tot_t += us

@@ -23,7 +23,7 @@ namespace {
 
 using namespace vrvq_conv;
 
-template <int BM, int BN, int WM, int NW, int KS, bool X3>
+template <int BM, int BN, int WM, int NW, int KS, bool X3, bool PH = false>
 __global__ __launch_bounds__(64 * NW)
 __attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
 void conv_mfma_kernel(ConvArgs a) {
@@ -52,7 +52,7 @@ void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TC::RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH>(a, smem, acc, b, m0, n0);
   else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
 }
@@ -295,6 +295,20 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
         x3_tile_ok(BM, BN, KS, a)) {
+      if constexpr (KS == 2) {
+        if (a.psh) {  // strided conv through the phase-split view
+          if (lx > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute(
+                (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
+            if (e != hipSuccess) return (int)e;
+          }
+          hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true>),
+                             dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
+          return vrvq_launch_status();
+        }
+      }
+      if (a.psh) return VRVQ_ERR_UNSUPPORTED;
       if (lx > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);

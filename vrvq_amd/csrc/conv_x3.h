@@ -90,7 +90,9 @@ struct X3W {
 // K loop of the implicit GEMM on the split operands. Same contract as conv_mainloop (acc zero
 // on entry, holds W * Xs of the tile on exit, ends after a barrier with every LDS stage free);
 // stride-1 windows only (a.ssh == 0), a.w3 = the pre-split weight.
-template <int BM, int BN, int WM, int NW, int KS>
+// PH: the phase-split view of a strided conv (ConvArgs::psh > 0; compile-time, so the stride-1
+// instantiations keep their plain window addressing).
+template <int BM, int BN, int WM, int NW, int KS, bool PH = false>
 __device__ __forceinline__ void conv_mainloop_x3(
     const ConvArgs& a, float* smem,
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
@@ -113,9 +115,9 @@ __device__ __forceinline__ void conv_mainloop_x3(
   const u32x4* w3 = reinterpret_cast<const u32x4*>(a.w3);
   // phase-split view (strided convs, a.psh > 0): view channel cv = c*s + r, position m reads
   // x[c][m*s + r - ppad]; with psh = 0 the same expressions reduce to x[cv][m]
-  const int psh = a.psh, pmask = (1 << psh) - 1, ppad = a.ppad;
-  const int ptin = psh ? a.ptin : a.tin;
-  const float* xb = a.x + (size_t)b * (psh ? (size_t)a.pcin * a.ptin : (size_t)a.cin * a.tin);
+  const int psh = PH ? a.psh : 0, pmask = (1 << psh) - 1, ppad = PH ? a.ppad : 0;
+  const int ptin = PH ? a.ptin : a.tin;
+  const float* xb = a.x + (size_t)b * (PH ? (size_t)a.pcin * a.ptin : (size_t)a.cin * a.tin);
   const int xbase = n0 - a.pad;
   const int nitems = NC8 * XW;
   char* sbase = reinterpret_cast<char*>(smem);
@@ -152,8 +154,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int cv = min(cb + u, a.cin - 1);
-        const int tp = min(max((tc << psh) + (cv & pmask) - ppad, 0), ptin - 1);
-        xr[it][u] = xb[(size_t)(cv >> psh) * ptin + tp];
+        if constexpr (PH) {
+          const int tp = min(max((tc << psh) + (cv & pmask) - ppad, 0), ptin - 1);
+          xr[it][u] = xb[(size_t)(cv >> psh) * ptin + tp];
+        } else {
+          xr[it][u] = xb[(size_t)cv * a.tin + tc];
+        }
       }
     }
   };
@@ -170,13 +176,17 @@ __device__ __forceinline__ void conv_mainloop_x3(
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int cv = ci0 + c8 * 8 + u;
-        const int tp = (t << psh) + (cv & pmask) - ppad;  // = t without the view
-        v[u] = (okp && cv < a.cin && tp >= 0 && tp < ptin) ? xr[it][u] : 0.0f;
+        bool ok = okp && cv < a.cin;
+        if constexpr (PH) {
+          const int tp = (t << psh) + (cv & pmask) - ppad;
+          ok = ok && tp >= 0 && tp < ptin;
+        }
+        v[u] = ok ? xr[it][u] : 0.0f;
       }
       if (a.alpha != nullptr) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int ci = min(ci0 + c8 * 8 + u, a.cin - 1) >> psh;
+          const int ci = PH ? min(ci0 + c8 * 8 + u, a.cin - 1) >> psh : min(ci0 + c8 * 8 + u, a.cin - 1);
           v[u] = snake_act(v[u], a.alpha[ci], a.inv_alpha[ci]);  // snake(0) = 0
         }
       }
