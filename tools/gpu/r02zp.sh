@@ -1,0 +1,22 @@
+#!/bin/bash
+# RVQ: chain scan with packed fma / add, projection folded into the chain prologue (nq <= 16):
+# smoke, GPU suite, RVQ micro-bench fold on / off (configs 2 and 3), rocprof kernel stats,
+# end-to-end bench fold on / off.
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-run}
+run() { local name=$1 to=$2; shift 2
+  echo "=== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1; local rc=$?
+  echo "=== $name rc=$rc"; grep -o '"value": [0-9.]*\|[0-9]* passed.*\|[0-9]* failed.*\|\[smoke\].*\|rvq_encode median.*' "gpurun_out/${TAG}_$name.log" | tail -3
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; grep -E "Error|assert|FAILED" "gpurun_out/${TAG}_$name.log" | head -20; exit $rc; fi; return 0; }
+run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+run pytest_fold 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rf --timeout 120 --timeout-method thread -k "fold or rvq"
+run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread
+run rvq_b32 120 python tools/rvq_bench.py
+run rvq_b32_nofold 120 env VRVQ_RVQ_FOLD=0 python tools/rvq_bench.py
+run rvq_b64 120 python tools/rvq_bench.py --batch 64 --nq 32
+run rvq_prof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/rvqprof_$TAG -o run --output-format csv -- python tools/rvq_bench.py --iters 20
+run bench 400 python bench.py --steps 20 --warmup 3
+run bench_nofold 300 env VRVQ_RVQ_FOLD=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline
+exit 0

@@ -42,6 +42,7 @@ constexpr int CH_NW = CH_NT / 64;
 constexpr int CH_FMAX = 16;     // frames per chain workgroup
 constexpr int CH_NQMAX = 32;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -426,25 +427,32 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
       for (int t = 0; t < NT; ++t)
         d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, d[t], 0, 0, 0);
       float bst[4];
-      int bix[4];
+      int bix[4];  // 16 t of the best entry (a constant per entry: no per-entry index add)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         bst[r] = INFINITY;
-        bix[r] = cw + 4 * lg + r;
+        bix[r] = 0;
       }
+      const f32x2 m2 = {-2.0f, -2.0f}, e22 = {e2, e2};
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const float ccv[4] = {cc[t].x, cc[t].y, cc[t].z, cc[t].w};
+        // (sum e^2 - 2 e.c) + sum c^2 with the first step as fma(d, -2, e2): 2d is exact,
+        // so this is the reference's rounding (models/quantize.py:96-100); two entries per
+        // packed fma / add (v_pk_fma_f32, v_pk_add_f32: the same per-element roundings)
+        const f32x2 d01 = {d[t][0], d[t][1]}, d23 = {d[t][2], d[t][3]};
+        const f32x2 c01 = {cc[t].x, cc[t].y}, c23 = {cc[t].z, cc[t].w};
+        const f32x2 s01 = __builtin_elementwise_fma(d01, m2, e22) + c01;
+        const f32x2 s23 = __builtin_elementwise_fma(d23, m2, e22) + c23;
+        const float dist[4] = {s01.x, s01.y, s23.x, s23.y};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // (sum e^2 - 2 e.c) + sum c^2 with the first step as fma(d, -2, e2): 2d is exact,
-          // so this is the reference's rounding (models/quantize.py:96-100)
-          const float dist = fmaf(d[t][r], -2.0f, e2) + ccv[r];
-          const bool take = dist < bst[r];  // increasing code index: strict < keeps the first
-          bst[r] = take ? dist : bst[r];
-          bix[r] = take ? cw + t * 16 + 4 * lg + r : bix[r];
+          const bool take = dist[r] < bst[r];  // increasing code index: strict < keeps the first
+          bst[r] = take ? dist[r] : bst[r];
+          bix[r] = take ? t * 16 : bix[r];
         }
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bix[r] += cw + 4 * lg + r;
       vrvq::amin(bst[0], bix[0], bst[1], bix[1]);
       vrvq::amin(bst[2], bix[2], bst[3], bix[3]);
       vrvq::amin(bst[0], bix[0], bst[2], bix[2]);
