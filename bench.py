@@ -6,6 +6,7 @@
     python bench.py [--gpus N --steps K --warmup W]                 configs[1] (default)
     python bench.py --batch 64 --n-codebooks 32                      configs[2] shape
     python bench.py --sweep [--batch 16]                             configs[4]: VBR level sweep
+    python bench.py --gpus N ...          N ranks (this script launches torch.distributed.run)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank/GPU)
 
 Multi-GPU: clips shard data-parallel (each rank its own clips, no data-path collective), weak
@@ -29,6 +30,8 @@ import glob
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -186,7 +189,7 @@ def cpu_baseline(kwargs, clips: int, runs: int = 3):
         shapes = {k: tuple(v.shape) for k, v in vrvq_amd.DAC_VRVQ(**kwargs).state_dict().items()}
         ref = TorchRef(recipe_state_dict(shapes, 0), **kwargs)
         audio = torch.from_numpy(synthetic_audio(clips, CLIP_SAMPLES, seed=1234))
-        ref.forward(audio[:1], 1.0)  # warm-up (allocator, MKLDNN primitive caches, threads)
+        ref.forward(audio, 1.0)  # warm-up at the timed shape (allocator, MKLDNN primitives)
         ts = []
         for _ in range(runs):
             t0 = time.perf_counter()
@@ -199,8 +202,8 @@ def cpu_baseline(kwargs, clips: int, runs: int = 3):
             "kind": "port", "implementation": "torch-restatement (oracle/torch_ref.py)",
             "cpu_model": cpu_model(), "median_of": runs,
             "sample": f"{clips} x 1 s clips of the same workload (B={clips} of 32), full "
-                      f"preprocess+encode+RVQ+decode, torch CPU, 1 warm-up, median of {runs} "
-                      f"runs ({', '.join(f'{t:.2f}' for t in ts)} s)"}
+                      f"preprocess+encode+RVQ+decode, torch CPU, 1 warm-up at B={clips}, "
+                      f"median of {runs} runs ({', '.join(f'{t:.2f}' for t in ts)} s)"}
 
 
 def build_model(args, dev):
@@ -255,7 +258,51 @@ def train_main(args, world: int, rank: int, dev):
             "losses_last_step_rank0": losses}), flush=True)
 
 
-def main():
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`--gpus N` run started as a plain `python bench.py`: launch N ranks of this script, one
+    process per GPU, the way the reference launches its multi-GPU jobs
+    (scripts/script_train.sh:33: torch.distributed.run --nproc_per_node). torch.distributed.run
+    sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, each rank binds cuda:LOCAL_RANK and joins the
+    RCCL process group, and rank 0 prints the job's JSON line. This parent only waits: it never
+    initialises the GPU, and it starts the ranks as children (no exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_main(args, world: int, rank: int) -> None:
+    """The launcher and the timed-region contract without a GPU (tests/test_bench_launcher.py):
+    gloo process group, a stub CPU step, barrier-bracketed timing with the MAX over ranks, and
+    the count of ranks that ran (a SUM all-reduce), reported by rank 0 as one JSON line."""
+    from vrvq_amd.replicas import sum_over_ranks, throughput, timed_steps
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.full((64, 64), 1.0 / 64)
+
+    def step():
+        return float((x @ x).sum())
+
+    res_t = timed_steps(step, args.steps, args.warmup)
+    ranks_seen = int(sum_over_ranks([1.0])[0])
+    if rank == 0:
+        print(json.dumps({"metric": "selftest", "value": round(throughput(1.0, res_t), 3),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ranks_seen": ranks_seen,
+                          "ms_per_step": round(res_t.seconds / args.steps * 1e3, 3)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -267,15 +314,26 @@ def main():
     ap.add_argument("--train", action="store_true",
                     help="configs[3]: vrvq_a2 training step (generator + discriminator + losses, "
                          "DDP over RCCL), 0.38 s clips")
-    ap.add_argument("--cpu-clips", type=int, default=4)
+    ap.add_argument("--cpu-clips", type=int, default=32,
+                    help="clips of the cpu_baseline sample (BASELINE.md: the full B=32 batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher / timing self-test: gloo on CPU with a stub step, no GPU")
+    args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 16 if args.sweep else 32
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks ourselves. Nothing
+        # in this process has touched the GPU (torch.cuda is not initialised by the import).
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
+    if args.selftest:
+        return selftest_main(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))

@@ -357,7 +357,8 @@ int vrvq_pack_conv1d_flip(const float* w, int cout, int cin, int k, int cin_pad,
                           float* w_packed, vrvq_stream_t stream);
 
 /* Training-mode importance mask (models/quantize.py:377-414, models/utils.py:11-61): rows
- * b < n_imps: generate_mask_ste((imp * levels[b]) * nq, alpha) (value smooth + (hard - smooth));
+ * b < n_imps: generate_mask_ste((imp * levels[b]) * nq, alpha) (value smooth + (hard - smooth)),
+ * or, with levels == NULL, generate_mask_ste(imp, alpha) of an already scaled map;
  * the next n_drop rows n_imps + j: generate_mask_hard(dropout[j]) (the first n_drop draws, as
  * models/quantize.py:412-413 assigns dropout[:n_dropout]); the rest 1. imp [B][T], levels [B],
  * dropout [B] int64 (may be NULL when n_drop = 0), mask [B][nq][T]. */
@@ -365,7 +366,7 @@ int vrvq_mask_ste(const float* imp, const float* levels, const int64_t* dropout,
                   int frames, int nq, float alpha, int n_imps, int n_drop, float* mask,
                   vrvq_stream_t stream);
 /* Its backward: dimp[b][t] = (sum_i dmask[b][i][t] logcosh'(x - i)) * nq * levels[b] for
- * b < n_imps, 0 for the overwritten rows. */
+ * b < n_imps (without the * nq * levels[b] when levels == NULL), 0 for the overwritten rows. */
 int vrvq_mask_ste_backward(const float* imp, const float* levels, const float* dmask, int batch,
                            int frames, int nq, float alpha, int n_imps, float* dimp,
                            vrvq_stream_t stream);

@@ -93,6 +93,29 @@ def test_wav_roundtrip(tmp_path):
     assert float((s.audio_data - x).abs().max()) < 1.0 / 32767 + 1e-6
 
 
+def test_decompress_rejects_out_of_range_codes():
+    """A code >= codebook_size is the VBR mask marker only for a VBR quantizer (== size); a CBR
+    model, a larger code or a negative one is a corrupt container: ValueError naming the code,
+    raised before any decode."""
+    from vrvq_amd.codes_io import DACFile
+    codes = torch.zeros(1, 8, 10, dtype=torch.long)
+    codes[0, 3, 4] = 1024
+
+    def dac(c):
+        return DACFile(codes=c, chunk_length=10, original_length=5120,
+                       input_db=np.array([-20.0], np.float32), channels=1, sample_rate=SR,
+                       padding=True, dac_version="1.0.0")
+    cbr = vrvq_amd.DAC_VRVQ(**{**KW, "model_type": "CBR"})
+    with pytest.raises(ValueError, match="VBR mask marker"):
+        cbr.decompress(dac(codes))
+    vbr = vrvq_amd.DAC_VRVQ(**KW)
+    for v in (1025, -1):
+        c = codes.clone()
+        c[0, 3, 4] = v
+        with pytest.raises(ValueError, match=f"code {v} is out of range"):
+            vbr.decompress(dac(c))
+
+
 # ------------------------------------------------------------------------------ restatement
 def _ref_compress(tr: TorchRef, model, audio, win_duration, level=1.0, normalize_db=-16.0):
     """models/dac_base.py:162-240 on the CPU restatement (VBR masks carried as codebook_size)."""

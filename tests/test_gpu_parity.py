@@ -199,6 +199,39 @@ def test_conv1d_vs_torch(case):
         assert rel_err(ys.cpu().numpy(), _snake_ref(y, a_next).cpu().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("mag", [1e3, 1e5, 1e7])
+def test_snake_large_arguments(mag):
+    """Snake (models/layers.py:26-32) for |alpha x| in [0.67, 1.33] * mag: the conv prologue
+    (fp32 and x3 paths), the producer-side epilogue Snake and the Snake backward against fp64
+    evaluated at the fp32 product u = fl(alpha * x) -- what the reference's fp32 torch.sin sees.
+    Past 2^20 the kernels' Cody-Waite reduction hands over to the Payne-Hanek sinf."""
+    gen = torch.Generator(device="cpu").manual_seed(int(mag) & 0xFFFF)
+    C, T = 16, 300
+    x = (torch.rand(2, C, T, generator=gen) * 0.5 + 0.5) * torch.sign(torch.rand(2, C, T, generator=gen) - 0.5)
+    alpha = (torch.rand(C, generator=gen) * 0.1 + 0.95) * mag
+    xd, ad = x.to(DEV), alpha.to(DEV)
+    ia = ops.snake_inv_alpha(ad)
+    u = (alpha.reshape(1, -1, 1) * x).double()          # fp32 product, then exact sin / cos
+    inv = (alpha.double() + 1e-9).reciprocal().reshape(1, -1, 1)
+    snk64 = x.double() + inv * torch.sin(u).pow(2)
+    w = torch.eye(C).reshape(C, C, 1).to(DEV)
+    wp, cp = ops.pack_conv1d_weight(w)
+    for w3 in (None, ops.pack_x3_weight(wp, 1)):
+        y = ops.conv1d(xd, wp, C, cp, 1, 1, 0, 1, alpha=ad, inv_alpha=ia, w_x3=w3)
+        assert rel_err(y.cpu().numpy(), snk64.numpy()) < 1e-5
+    # producer-side Snake of the next layer (epilogue) with the large alpha
+    _, ys = ops.conv1d(xd, wp, C, cp, 1, 1, 0, 1, out_snake=(ad, ia), want_raw=False)
+    assert rel_err(ys.cpu().numpy(), snk64.numpy()) < 1e-6
+    # backward: dx = g (1 + inv 2 sin cos alpha), dalpha = sum g (-inv^2 sin^2 + inv 2 sin cos x)
+    g = torch.randn(2, C, T, generator=gen)
+    s2 = 2 * torch.sin(u) * torch.cos(u)
+    dx64 = g.double() * (1 + inv * s2 * alpha.double().reshape(1, -1, 1))
+    da64 = (g.double() * (-(inv * inv) * torch.sin(u).pow(2) + inv * s2 * x.double())).sum((0, 2))
+    dx, da = ops.snake_backward(xd, ad, ia, g.to(DEV))
+    assert rel_err(dx.cpu().numpy(), dx64.numpy()) < 1e-5
+    assert rel_err(da.cpu().numpy(), da64.numpy()) < 1e-4
+
+
 @pytest.mark.parametrize("k,p", [(7, 3), (3, 1)])
 def test_cout1_stream_matches_small_kernel(k, p):
     """The Cout = 1 stream kernel (tin % 4 == 0) and the LDS-staged small-Cout kernel (other

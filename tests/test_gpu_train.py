@@ -163,6 +163,30 @@ def test_mask_ste_vs_torch64():
     assert l2rel(impd.grad.cpu().numpy(), imp64.grad.numpy()) < TOL
 
 
+def test_generate_mask_ste_public_vs_torch64():
+    """vrvq_amd.generate_mask_ste (the public helper, models/utils.py:45-53) is differentiable:
+    hard-mask forward, log-cosh backward, against the fp64 restatement."""
+    B, T, nq, alpha = 3, 61, 8, 2.0
+    g0 = torch.Generator().manual_seed(21)
+    x = torch.rand(B, 1, T, generator=g0) * (nq + 2) - 1.0
+    x64 = x.double().requires_grad_()
+    pm = x64 - torch.arange(nq, dtype=torch.float64)[None, :, None]
+    sm = logcosh64(alpha, pm)
+    m64 = sm + ((pm >= 0).double() - sm).detach()
+    gm = torch.randn(B, nq, T, generator=g0)
+    (m64 * gm.double()).sum().backward()
+    xd = x.to(DEV).requires_grad_()
+    m = vrvq_amd.generate_mask_ste(xd, nq, alpha)
+    np.testing.assert_array_equal(m.detach().cpu().numpy(), m64.detach().numpy())
+    np.testing.assert_array_equal(m.detach().cpu().numpy(),
+                                  vrvq_amd.generate_mask_hard(x.to(DEV), nq).cpu().numpy())
+    (m * gm.to(DEV)).sum().backward()
+    assert l2rel(xd.grad.cpu().numpy(), x64.grad.numpy()) < TOL
+    with torch.no_grad():  # no tape: the plain hard-mask kernel
+        np.testing.assert_array_equal(vrvq_amd.generate_mask_ste(xd, nq, alpha).cpu().numpy(),
+                                      m64.detach().numpy())
+
+
 # ------------------------------------------------------------------ quantizer backward
 def rvq64(z, mask, g_in, v_in, b_in, g_out, v_out, b_out, cb, codes):
     """The reference quantizer loop (models/quantize.py:42-79, 353-423) in fp64 autograd with the
@@ -218,6 +242,106 @@ def test_rvq_backward_vs_torch64(nq, B, T):
     for nm, a, r in zip(names, leaves, leaves64):
         e = l2rel(a.grad.cpu().numpy(), r.grad.numpy())
         assert e < TOL, f"{nm}: rel {e}"
+
+
+def _quantizer_leaves(q):
+    leaves = [a.detach().double().cpu().requires_grad_() for a in train._stage_params(q.quantizers)]
+    return leaves
+
+
+def _check_quantizer_train(q, z, out, mask_ref):
+    """z_q / losses / gradients of a training-mode quantizer output against rvq64 with the
+    reference's mask (codes fixed, as the straight-through estimator uses them)."""
+    leaves64 = _quantizer_leaves(q)
+    z64 = z.detach().double().cpu().requires_grad_()
+    zq64, c64, cb64 = rvq64(z64, mask_ref.double(), *leaves64, out["codes"].cpu())
+    assert rel_err(out["z_q"].detach().cpu().numpy(), zq64.detach().numpy()) < TOL
+    assert float(out["commitment_loss"]) == pytest.approx(float(c64), rel=TOL)
+    assert float(out["codebook_loss"]) == pytest.approx(float(cb64), rel=TOL)
+    g0 = torch.Generator().manual_seed(77)
+    gz = torch.randn(z.shape, generator=g0)
+    (zq64 * gz.double()).sum().add(0.25 * c64 + cb64).backward()
+    ((out["z_q"] * gz.to(DEV)).sum() + 0.25 * out["commitment_loss"]
+     + out["codebook_loss"]).backward()
+    assert l2rel(z.grad.cpu().numpy(), z64.grad.numpy()) < TOL
+    names = ["g_in", "v_in", "b_in", "g_out", "v_out", "b_out", "cb"]
+    got = [torch.cat([qq.in_proj.weight_g.grad.reshape(-1) for qq in q.quantizers]),
+           torch.cat([qq.in_proj.weight_v.grad.reshape(qq.in_proj.out_channels, -1)
+                      for qq in q.quantizers]),
+           torch.stack([qq.in_proj.bias.grad for qq in q.quantizers]),
+           torch.cat([qq.out_proj.weight_g.grad.reshape(-1) for qq in q.quantizers]),
+           torch.cat([qq.out_proj.weight_v.grad.reshape(qq.out_proj.out_channels, -1)
+                      for qq in q.quantizers]),
+           torch.stack([qq.out_proj.bias.grad for qq in q.quantizers]),
+           torch.stack([qq.codebook.weight.grad for qq in q.quantizers])]
+    for nm, a, r in zip(names, got, leaves64):
+        e = l2rel(a.cpu().numpy(), r.grad.numpy())
+        assert e < TOL, f"{nm}: rel {e}"
+
+
+def _random_quantizer(q, seed):
+    g0 = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in q.named_parameters():
+            if "codebook" in name:
+                p.copy_(torch.randn(p.shape, generator=g0))
+            elif "weight_g" in name:
+                p.copy_(torch.rand(p.shape, generator=g0) + 0.5)
+            elif "weight_v" in name:
+                p.copy_(torch.randn(p.shape, generator=g0) * (0.03 if "in_proj" in name else 0.3))
+            else:
+                p.copy_(torch.randn(p.shape, generator=g0) * 0.1)
+    return q.to(DEV).train()
+
+
+def test_cbr_train_quantizer_vs_torch64():
+    """ResidualVectorQuantize in training mode with quantizer dropout (models/quantize.py:165-214):
+    row b keeps stages i < n_quantizers[b] for the first int(B * dropout) rows (randint draws
+    under the same seed), all stages otherwise."""
+    from vrvq_amd.model import ResidualVectorQuantize
+    nq, B, T = 5, 6, 37
+    q = _random_quantizer(ResidualVectorQuantize(input_dim=1024, n_codebooks=nq,
+                                                 codebook_size=1024, codebook_dim=8,
+                                                 quantizer_dropout=0.5), 31)
+    z = (torch.randn(B, 1024, T, generator=torch.Generator().manual_seed(32)) * 0.5).to(DEV)
+    z.requires_grad_()
+    torch.manual_seed(123)
+    out = q(z)
+    torch.manual_seed(123)  # the reference's draws (models/quantize.py:176-179)
+    n_q = torch.ones((B,)) * nq + 1
+    dropout = torch.randint(1, nq + 1, (B,))
+    n_drop = int(B * 0.5)
+    n_q[:n_drop] = dropout[:n_drop]
+    mask_ref = (torch.arange(nq)[None, :, None] < n_q[:, None, None]).float().expand(B, nq, T)
+    assert 0 < int((mask_ref == 0).sum())  # some stages dropped under this seed
+    np.testing.assert_array_equal(out["dropout"].numpy(), dropout.numpy())
+    _check_quantizer_train(q, z, out, mask_ref)
+
+
+def test_vbr_quantizer_cbr_mode_train_vs_torch64():
+    """VBRResidualVectorQuantize in training mode with n_quantizers = Nq (models/quantize.py:
+    346-414): mask rows ones / dropout / full codebook, no level draw, imp_map None."""
+    from vrvq_amd.model import VBRResidualVectorQuantize
+    nq, B, T = 6, 8, 29
+    q = _random_quantizer(VBRResidualVectorQuantize(
+        input_dim=1024, n_codebooks=nq, codebook_size=1024, codebook_dim=8, quantizer_dropout=0.5,
+        full_codebook_rate=0.25, level_min=0.125, level_max=6.0), 41)
+    z = (torch.randn(B, 1024, T, generator=torch.Generator().manual_seed(42)) * 0.5).to(DEV)
+    z.requires_grad_()
+    torch.manual_seed(7)
+    out = q(z, nq, None, None)
+    torch.manual_seed(7)
+    dropout = torch.randint(1, nq + 1, (B, 1, 1)).expand(B, 1, T)
+    n_full, n_drop = int(B * 0.25), int(B * 0.5)
+    n_imps = B - n_full - n_drop
+    mask_ref = torch.ones(B, nq, T)
+    mask_ref[n_imps:n_imps + n_drop] = (dropout[:n_drop] - torch.arange(nq)[None, :, None]
+                                        >= 0).float()
+    assert out["imp_map"] is None
+    np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), mask_ref.numpy())
+    with pytest.raises(RuntimeError):
+        q(z, nq - 1, None, None)
+    _check_quantizer_train(q, z, out, mask_ref)
 
 
 # ------------------------------------------------------------------ whole generator vs reference

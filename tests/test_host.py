@@ -92,8 +92,10 @@ def test_training_mode_cpu_fails_loudly():
     model.train()
     with pytest.raises(RuntimeError, match="GPU"):
         model.quantizer(torch.zeros(1, 1024, 4), None, torch.zeros(1, 1024, 4), 1)
-    with pytest.raises(NotImplementedError):  # VBR quantizer in CBR mode: eval only
+    with pytest.raises(RuntimeError, match="GPU"):  # VBR quantizer in CBR mode, training
         model.quantizer(torch.zeros(1, 1024, 4), 2, torch.zeros(1, 1024, 4), None)
+    with pytest.raises(RuntimeError, match="n_quantizers >= n_codebooks"):
+        model.quantizer(torch.zeros(1, 1024, 4), 1, torch.zeros(1, 1024, 4), None)
 
 
 def test_invalid_model_type():

@@ -132,3 +132,13 @@ def test_ddp_gradient_allreduce_gloo_world2():
 def test_a2_kwargs_match_reference_config(manifest):
     from vrvq_amd.config import A2_KWARGS
     assert A2_KWARGS == manifest["yml_kwargs"]["conf/vrvq/vrvq_a2.yml"]
+
+
+def test_unknown_lambda_key_raises():
+    """scripts/train.py:319 sums every lambda key: a misspelt key is a KeyError, raised before
+    any work; the VBR rate keys are accepted (a CBR model contributes no rate term)."""
+    from vrvq_amd.trainer import LAMBDAS_A2, check_lambdas
+    check_lambdas(LAMBDAS_A2)
+    check_lambdas({"mel/loss": 15.0, "vq/rate_loss": 2.0})
+    with pytest.raises(KeyError, match="mel/los"):
+        check_lambdas({**LAMBDAS_A2, "mel/los": 1.0})

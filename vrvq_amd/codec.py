@@ -280,11 +280,21 @@ def decompress(model, obj: Union[str, Path, DACFile], verbose: bool = False,
             raise RuntimeError("decompress: codes length is not a multiple of chunk_length")
         chunks = torch.cat(chunks, 0)                        # (n_win * items, nq, cl)
         n_cb = model.codebook_size
+        # VBR containers carry masked-out codes as the marker value codebook_size; only a VBR
+        # quantizer can decode them (from_codes with mask_imp). Anything else out of range is
+        # a corrupt file (or a VBR file given to a CBR model).
+        vbr = hasattr(model.quantizer, "imp_subnet")
+        bad = (chunks < 0) | (chunks > n_cb) | ((chunks == n_cb) & (not vbr))
+        if bool(bad.any()):
+            v = int(chunks[bad][0])
+            raise ValueError(f"decompress: code {v} is out of range for codebook_size {n_cb}"
+                             + ("" if vbr or v != n_cb else
+                                " (the VBR mask marker; this model's quantizer is CBR)"))
         recons = []
         for c0 in range(0, chunks.shape[0], max_batch):
             c = chunks[c0:c0 + max_batch].contiguous()
             mask = c < n_cb
-            if bool((~mask).any()):  # VBR container: codebook_size marks a masked-out code
+            if vbr and bool((~mask).any()):
                 z = model.quantizer.from_codes(torch.where(mask, c, torch.zeros_like(c)),
                                                mask_imp=mask.float())[0]
             else:

@@ -23,8 +23,15 @@ static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<h
 // < 7e-10). sin(u)^2 = sin(r)^2, so the quadrant sign is not needed. 14 VALU instead of the
 // ~40 of the general sinf (the mul of the reference's alpha * x is kept as is); max abs error
 // of the square 2.2e-7 (sinf: 1e-7) — within the parity tolerance, and the Snake-heavy
-// residual units spend most of their VALU here.
+// residual units spend most of their VALU here. For |u| >= 2^20 (and NaN / Inf) the three-term
+// reduction is no longer exact, so those lanes take sinf (ocml: Payne-Hanek reduction), which,
+// like the reference's torch.sin, is accurate for any argument; the test is one VALU compare and
+// the branch is skipped unless a lane of the wave needs it.
 __device__ __forceinline__ float sin_sq(float u) {
+  if (__builtin_expect(!(fabsf(u) < 0x1p20f), 0)) {
+    const float s = sinf(u);
+    return s * s;
+  }
   const float k = rintf(u * 0.318309886183790672f);
   float r = fmaf(-k, 3.14159274101257324e+00f, u);
   r = fmaf(-k, -8.74227765734758577e-08f, r);
@@ -42,8 +49,13 @@ __device__ __forceinline__ float sin_sq(float u) {
 
 // sin(r) and cos(r) of the reduced argument of u (r = u - k pi, |r| <= pi/2): sin(u) cos(u) =
 // sin(r) cos(r) and sin(u)^2 = sin(r)^2 (the (-1)^k signs cancel) -- what Snake's backward
-// needs. Same reduction as sin_sq; Taylor polynomials to degree 13 / 14.
+// needs. Same reduction as sin_sq; Taylor polynomials to degree 13 / 14. Same large-argument
+// guard as sin_sq (sincosf: the unreduced sin / cos have the same products).
 __device__ __forceinline__ void sincos_reduced(float u, float* sr, float* cr) {
+  if (__builtin_expect(!(fabsf(u) < 0x1p20f), 0)) {
+    sincosf(u, sr, cr);
+    return;
+  }
   const float k = rintf(u * 0.318309886183790672f);
   float r = fmaf(-k, 3.14159274101257324e+00f, u);
   r = fmaf(-k, -8.74227765734758577e-08f, r);

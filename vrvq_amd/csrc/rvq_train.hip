@@ -70,7 +70,9 @@ __global__ void mask_ste_kernel(const float* __restrict__ imp, const float* __re
     const int i = (int)(bi % nq), b = (int)(bi / nq);
     float m;
     if (b < n_imps) {
-      const float x = (imp[(size_t)b * T + t] * levels[b]) * (float)nq;
+      // levels == null: imp already holds the scaled map x (public generate_mask_ste)
+      const float x = levels ? (imp[(size_t)b * T + t] * levels[b]) * (float)nq
+                             : imp[(size_t)b * T + t];
       const float p = x - (float)i;
       const float sm = logcosh_smooth(p, alpha, ea);
       const float q = p >= 0.0f ? 1.0f : 0.0f;
@@ -85,6 +87,7 @@ __global__ void mask_ste_kernel(const float* __restrict__ imp, const float* __re
 }
 
 // dimp[b][t] = ((sum_i dmask[b][i][t] smooth'(p_i)) * nq) * level_b for b < n_imps, else 0
+// (levels == null: d/dx of the prescaled map, sum_i dmask smooth'(p_i))
 // (the dropout / full-codebook rows are overwritten in the reference: no gradient).
 __global__ void mask_ste_backward_kernel(const float* __restrict__ imp,
                                          const float* __restrict__ levels,
@@ -97,10 +100,10 @@ __global__ void mask_ste_backward_kernel(const float* __restrict__ imp,
     const int t = (int)(e % T), b = (int)(e / T);
     float g = 0.0f;
     if (b < n_imps) {
-      const float x = (imp[e] * levels[b]) * (float)nq;
+      const float x = levels ? (imp[e] * levels[b]) * (float)nq : imp[e];
       for (int i = 0; i < nq; ++i)
         g += dmask[((size_t)b * nq + i) * T + t] * logcosh_grad(x - (float)i, alpha, ea);
-      g = (g * (float)nq) * levels[b];
+      if (levels) g = (g * (float)nq) * levels[b];
     }
     dimp[e] = g;
   }
@@ -340,7 +343,7 @@ struct BwdWs {
 extern "C" int vrvq_mask_ste(const float* imp, const float* levels, const int64_t* dropout,
                              int batch, int frames, int nq, float alpha, int n_imps, int n_drop,
                              float* mask, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(imp && levels && mask && batch > 0 && frames > 0 && nq > 0 && alpha > 0.0f);
+  VRVQ_CHECK_ARG(imp && mask && batch > 0 && frames > 0 && nq > 0 && alpha > 0.0f);
   VRVQ_CHECK_ARG(n_imps >= 0 && n_drop >= 0 && n_imps + n_drop <= batch);
   VRVQ_CHECK_ARG(n_drop == 0 || dropout != nullptr);
   const float ea = (float)exp((double)alpha);  // math.exp(alpha), rounded to the tensor dtype
@@ -353,7 +356,7 @@ extern "C" int vrvq_mask_ste(const float* imp, const float* levels, const int64_
 extern "C" int vrvq_mask_ste_backward(const float* imp, const float* levels, const float* dmask,
                                       int batch, int frames, int nq, float alpha, int n_imps,
                                       float* dimp, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(imp && levels && dmask && dimp && batch > 0 && frames > 0 && nq > 0);
+  VRVQ_CHECK_ARG(imp && dmask && dimp && batch > 0 && frames > 0 && nq > 0);
   VRVQ_CHECK_ARG(alpha > 0.0f && n_imps >= 0 && n_imps <= batch);
   const float ea = (float)exp((double)alpha);
   hipLaunchKernelGGL(mask_ste_backward_kernel, dim3(grid_cap((size_t)batch * frames)), dim3(256),

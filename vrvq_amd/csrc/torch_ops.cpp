@@ -723,17 +723,19 @@ Tensor pack_conv1d_flip(const Tensor& w) {
 }
 
 // Training mask (models/quantize.py:377-414).
-Tensor mask_ste(const Tensor& imp, const Tensor& levels, const optional<Tensor>& dropout,
+Tensor mask_ste(const Tensor& imp, const optional<Tensor>& levels, const optional<Tensor>& dropout,
                 int64_t nq, double alpha, int64_t n_imps, int64_t n_drop) {
   check_t(imp, "imp");
-  check_on(levels, imp, "levels");
+  if (levels.has_value()) check_on(*levels, imp, "levels");
   if (dropout.has_value()) check_on(*dropout, imp, "dropout", at::kLong);
   const int64_t B = imp.size(0), T = imp.size(-1);
-  TORCH_CHECK(imp.numel() == B * T && levels.numel() == B, "mask_ste: imp (B, 1, T), levels (B)");
+  TORCH_CHECK(imp.numel() == B * T && (!levels.has_value() || levels->numel() == B),
+              "mask_ste: imp (B, 1, T), levels (B)");
   if (dropout.has_value()) TORCH_CHECK(dropout->numel() == B, "mask_ste: dropout (B)");
   c10::DeviceGuard guard(imp.device());
   Tensor mask = empty_f({B, nq, T}, imp);
-  check_rc(vrvq_mask_ste(imp.data_ptr<float>(), levels.data_ptr<float>(),
+  check_rc(vrvq_mask_ste(imp.data_ptr<float>(),
+                         levels.has_value() ? levels->data_ptr<float>() : nullptr,
                          dropout.has_value() ? dropout->data_ptr<int64_t>() : nullptr, (int)B,
                          (int)T, (int)nq, (float)alpha, (int)n_imps, (int)n_drop,
                          mask.data_ptr<float>(), stream_of(imp)),
@@ -741,17 +743,18 @@ Tensor mask_ste(const Tensor& imp, const Tensor& levels, const optional<Tensor>&
   return mask;
 }
 
-Tensor mask_ste_backward(const Tensor& imp, const Tensor& levels, const Tensor& dmask,
+Tensor mask_ste_backward(const Tensor& imp, const optional<Tensor>& levels, const Tensor& dmask,
                          double alpha, int64_t n_imps) {
   check_t(imp, "imp");
-  check_on(levels, imp, "levels");
+  if (levels.has_value()) check_on(*levels, imp, "levels");
   check_on(dmask, imp, "dmask");
   const int64_t B = imp.size(0), T = imp.size(-1);
   TORCH_CHECK(dmask.dim() == 3 && dmask.size(0) == B && dmask.size(2) == T,
               "mask_ste_backward: dmask (B, nq, T)");
   c10::DeviceGuard guard(imp.device());
   Tensor dimp = at::empty_like(imp);
-  check_rc(vrvq_mask_ste_backward(imp.data_ptr<float>(), levels.data_ptr<float>(),
+  check_rc(vrvq_mask_ste_backward(imp.data_ptr<float>(),
+                                  levels.has_value() ? levels->data_ptr<float>() : nullptr,
                                   dmask.data_ptr<float>(), (int)B, (int)T, (int)dmask.size(1),
                                   (float)alpha, (int)n_imps, dimp.data_ptr<float>(),
                                   stream_of(imp)),
@@ -911,10 +914,10 @@ TORCH_LIBRARY(vrvq, m) {
   m.def("weight_norm_backward(Tensor g, Tensor v, Tensor dw) -> (Tensor, Tensor)");
   m.def("pack_conv1d_flip(Tensor w) -> Tensor");
   m.def(
-      "mask_ste(Tensor imp, Tensor levels, Tensor? dropout, int nq, float alpha, int n_imps, "
+      "mask_ste(Tensor imp, Tensor? levels, Tensor? dropout, int nq, float alpha, int n_imps, "
       "int n_drop) -> Tensor");
   m.def(
-      "mask_ste_backward(Tensor imp, Tensor levels, Tensor dmask, float alpha, int n_imps) "
+      "mask_ste_backward(Tensor imp, Tensor? levels, Tensor dmask, float alpha, int n_imps) "
       "-> Tensor");
   m.def(
       "rvq_encode_train(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "

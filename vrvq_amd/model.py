@@ -302,8 +302,8 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
         if n_quantizers is None and level is None:
             raise AssertionError("level must be specified in VBR mode")
         if self.training:
-            if n_quantizers is not None:
-                raise NotImplementedError("VBR quantizer in CBR mode is eval-only")
+            if n_quantizers is not None:  # CBR mode: ones + dropout / full rows (:397-414)
+                return train.vbr_cbr_forward(self, z.contiguous(), n_quantizers)
             # random levels / dropout / full-codebook rows, autograd (models/quantize.py:374-414)
             return train.vbr_forward(self, z.contiguous(), feat_enc.contiguous())
         B, D, T = z.shape

@@ -180,6 +180,7 @@ class _MaskSte(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, imp, levels, dropout, nq, alpha, n_imps, n_drop):
+        # levels None: imp is already the scaled map x of generate_mask_ste(x, nq, alpha)
         B, T = imp.shape[0], imp.shape[-1]
         imp2 = imp.detach().reshape(B, T).contiguous()
         mask = ops.mask_ste(imp2, levels, dropout, nq, alpha, n_imps, n_drop)
@@ -297,6 +298,41 @@ def vbr_forward(q, z, feat):
             "commitment_loss": commit, "codebook_loss": cbl,
             "imp_map": imp_map[:n_imps], "mask_imp": mask,
             "random_levels": levels, "dropout": dropout}
+
+
+def mask_ste(x: torch.Tensor, nq: int, alpha: float = 1.0) -> torch.Tensor:
+    """generate_mask_ste(x, nq, alpha) of models/utils.py:45-53 with its backward: x (B, 1, T)
+    the scaled importance map; forward the hard mask, backward d logcosh(alpha, x - n) / dx."""
+    if x.dim() != 3 or x.shape[1] != 1:
+        raise RuntimeError(f"generate_mask_ste: x must be (B, 1, T), got {tuple(x.shape)}")
+    return _MaskSte.apply(x, None, None, int(nq), float(alpha), int(x.shape[0]), 0)
+
+
+def vbr_cbr_forward(q, z, n_quantizers: int):
+    """VBRResidualVectorQuantize.forward in training mode with n_quantizers given (CBR mode,
+    models/quantize.py:346-414): every stage runs, the importance rows of the mask are ones
+    (no level draw, no importance map), then the dropout and full-codebook rows. The only draw
+    is the dropout randint (:406). n_quantizers < Nq fails in the reference (shape mismatch
+    at :421) and raises here."""
+    B, D, T = z.shape
+    nq = q.n_codebooks
+    if int(n_quantizers) < nq:
+        raise RuntimeError(
+            f"VBRResidualVectorQuantize in CBR mode needs n_quantizers >= n_codebooks "
+            f"({n_quantizers} < {nq}), as in the reference")
+    dropout = torch.randint(1, nq + 1, (B, 1, 1))
+    n_full = int(B * q.full_codebook_rate)
+    n_drop = int(B * q.quantizer_dropout)
+    n_imps = int(B) - n_full - n_drop
+    dev = z.device
+    # rows < n_imps: mask_imp = ones (:400) -- the STE of the constant map x = nq is 1 exactly
+    ones = torch.full((B, T), float(nq), device=dev)
+    mask = ops.mask_ste(ones, None, dropout.reshape(B).to(dev).contiguous(), nq, 1.0,
+                        max(n_imps, 0), n_drop)
+    z_q, commit, cbl, codes, lat = _rvq(q.quantizers, z, mask)
+    return {"z_q": z_q, "z_q_is": None, "codes": codes, "latents": lat,
+            "commitment_loss": commit, "codebook_loss": cbl, "imp_map": None,
+            "mask_imp": mask, "dropout": dropout}
 
 
 def cbr_forward(q, z):

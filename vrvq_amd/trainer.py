@@ -70,12 +70,28 @@ def build_state(generator: DAC_VRVQ, device: torch.device, ddp: bool = False,
                  gan_loss=GANLoss(disc), waveform_loss=L1Loss())
 
 
+LOSS_KEYS = ("adv/disc_loss", "stft/loss", "mel/loss", "waveform/loss", "adv/gen_loss",
+             "adv/feat_loss", "vq/commitment_loss", "vq/codebook_loss")
+RATE_KEYS = ("vq/rate_loss", "vq/rate_loss_scaled")
+
+
+def check_lambdas(lambdas: Dict[str, float]) -> None:
+    """scripts/train.py:319 sums `v * output[k]` over every lambda key, so a key with no loss
+    term is a KeyError there; raised here before any work. The one allowance: the rate terms of
+    a VBR lambda set on a CBR model (no importance map), which contribute nothing."""
+    known = set(LOSS_KEYS) | set(RATE_KEYS)
+    missing = [k for k in lambdas if k not in known]
+    if missing:
+        raise KeyError(f"train_step: lambda keys with no loss term: {missing}")
+
+
 def train_step(state: State, audio: torch.Tensor, lambdas: Dict[str, float] = LAMBDAS_A2,
                sample_rate: int = 44100) -> Dict[str, torch.Tensor]:
     """One iteration of scripts/train.py:262-335 on a (B, 1, T) batch already on the device:
     generator forward (train mode), discriminator update, generator losses + update. Returns the
     loss / norm tensors (device tensors: no host sync here)."""
     gen, disc = state.generator, state.discriminator
+    check_lambdas(lambdas)
     gen.train()
     disc.train()
     n_codebooks = unwrap(gen).n_codebooks

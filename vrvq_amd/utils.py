@@ -22,12 +22,18 @@ def generate_mask_hard(x: torch.Tensor, nq: int) -> torch.Tensor:
 
 
 def generate_mask_ste(x: torch.Tensor, nq: int, alpha: float = 1) -> torch.Tensor:
-    """Forward value of the straight-through mask (models/utils.py:45-53).
+    """Straight-through mask (models/utils.py:45-53): x (B, 1, T) the scaled importance map.
 
-    mask_smooth + (mask_quant - mask_smooth).detach() equals the hard mask exactly in fp32
-    (for q = 0 it is s + (-s) = 0; for q = 1, s >= 0.5 and 1 - s is exact by Sterbenz), so the
-    forward pass is the hard-mask kernel; the log-cosh backward belongs to the training row."""
-    return ops.mask_hard(_as_scaled(x), nq)
+    Forward: mask_smooth + (mask_quant - mask_smooth).detach(), which equals the hard mask
+    exactly in fp32 (for q = 0 it is s + (-s) = 0; for q = 1, s >= 0.5 and 1 - s is exact by
+    Sterbenz). Backward (when x requires grad): d/dx of the log-cosh smooth step
+    logcosh(alpha, x - n) (models/utils.py:11-32), summed over the nq rows. Both run in the
+    mask STE kernels (include/vrvq.h vrvq_mask_ste with levels = NULL)."""
+    from . import train
+    x = _as_scaled(x)
+    if x.requires_grad and torch.is_grad_enabled():
+        return train.mask_ste(x, nq, float(alpha))
+    return ops.mask_hard(x, nq)
 
 
 def scale_importance(imp_map: torch.Tensor, a: float, c: float = 1.0) -> torch.Tensor:
