@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--nq", type=int, default=8)
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -37,16 +38,19 @@ def main():
     imp = torch.rand(args.batch, args.frames, generator=g).to(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
+    run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
+                                 want_z_q_is=not args.no_zqis)
     for it in range(args.iters):
         e0.record()
-        ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+        run()
         e1.record()
         torch.cuda.synchronize()
         if it >= min(5, args.iters - 1):
             ts.append(e0.elapsed_time(e1) * 1e3)
     med = sorted(ts)[len(ts) // 2]
     byt = rvq_bytes(args.batch, args.frames, args.nq)
-    print(f"B={args.batch} nq={args.nq} T={args.frames}: rvq_encode median {med:.1f} us "
+    tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
+    print(f"B={args.batch} nq={args.nq} T={args.frames}: {tag} median {med:.1f} us "
           f"(min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
           f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB")
 

@@ -23,15 +23,8 @@ static inline hipStream_t as_stream(vrvq_stream_t s) { return reinterpret_cast<h
 // < 7e-10). sin(u)^2 = sin(r)^2, so the quadrant sign is not needed. 14 VALU instead of the
 // ~40 of the general sinf (the mul of the reference's alpha * x is kept as is); max abs error
 // of the square 2.2e-7 (sinf: 1e-7) — within the parity tolerance, and the Snake-heavy
-// residual units spend most of their VALU here. For |u| >= 2^20 (and NaN / Inf) the three-term
-// reduction is no longer exact, so those lanes take sinf (ocml: Payne-Hanek reduction), which,
-// like the reference's torch.sin, is accurate for any argument; the test is one VALU compare and
-// the branch is skipped unless a lane of the wave needs it.
-__device__ __forceinline__ float sin_sq(float u) {
-  if (__builtin_expect(!(fabsf(u) < 0x1p20f), 0)) {
-    const float s = sinf(u);
-    return s * s;
-  }
+// residual units spend most of their VALU here. No range check: see snake_n / sin_sq.
+__device__ __forceinline__ float sin_sq_fast(float u) {
   const float k = rintf(u * 0.318309886183790672f);
   float r = fmaf(-k, 3.14159274101257324e+00f, u);
   r = fmaf(-k, -8.74227765734758577e-08f, r);
@@ -45,6 +38,22 @@ __device__ __forceinline__ float sin_sq(float u) {
   p = fmaf(p, r2, -1.6666666666666667e-01f);    // -1/3!
   const float s = fmaf(r * r2, p, r);
   return s * s;
+}
+
+// Arguments the reduction above does not take: |u| >= 2^20, NaN, Inf. Those go to sinf (ocml:
+// Payne-Hanek reduction), which, like the reference's torch.sin, is accurate for any argument.
+__device__ __forceinline__ bool snake_arg_big(float u) { return !(fabsf(u) < 0x1p20f); }
+
+__device__ __forceinline__ float sin_sq_exact(float u) {
+  const float s = sinf(u);
+  return s * s;
+}
+
+// Single value with its own range check (an exec-masked branch per element: for the cold
+// paths; the hot loops use snake_n).
+__device__ __forceinline__ float sin_sq(float u) {
+  if (__builtin_expect(snake_arg_big(u), 0)) return sin_sq_exact(u);
+  return sin_sq_fast(u);
 }
 
 // sin(r) and cos(r) of the reduced argument of u (r = u - k pi, |r| <= pi/2): sin(u) cos(u) =
@@ -82,6 +91,41 @@ __device__ __forceinline__ void sincos_reduced(float u, float* sr, float* cr) {
 // The reference's op sequence (mul, sin, square, mul, add); sin^2 from sin_sq.
 __device__ __forceinline__ float snake_act(float v, float alpha, float inv_alpha) {
   return v + inv_alpha * sin_sq(alpha * v);
+}
+
+// Snake on N values at once (the hot staging / epilogue loops): the fast reduction for all of
+// them, and one wave-uniform branch for the group -- taken only when a lane of the wave holds an
+// argument past the reduction's range, and then only those elements take sinf. Per element this
+// costs one compare (the per-element branch of sin_sq split every element into its own block and
+// cost the residual units 5-8 %). Same values as snake_act, element for element.
+template <int N>
+__device__ __forceinline__ void snake_n(float (&v)[N], const float (&al)[N], const float (&ia)[N]) {
+  float u[N], s[N];
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    u[i] = al[i] * v[i];
+    big = big || snake_arg_big(u[i]);
+    s[i] = sin_sq_fast(u[i]);
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(big) != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = snake_arg_big(u[i]) ? sin_sq_exact(u[i]) : s[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = v[i] + ia[i] * s[i];
+}
+
+// ... with one alpha for the whole group
+template <int N>
+__device__ __forceinline__ void snake_n1(float (&v)[N], float alpha, float inv_alpha) {
+  float al[N], ia[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    al[i] = alpha;
+    ia[i] = inv_alpha;
+  }
+  snake_n<N>(v, al, ia);
 }
 
 // 8-term dot product in k order (fmaf chain); used for in_proj/out_proj/codebook distance.

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
 // channel, then tap -- conv_small_cout_kernel's fmaf chain, so the two agree bit for bit.
 constexpr int C1_T = 4;
 constexpr int C1_W = 12;  // window samples per channel
-template <int KS, int PAD>
+template <int KS, int PAD, bool SNK>
 __global__ __launch_bounds__(256) void conv_cout1_stream_kernel(ConvArgs a) {
   static_assert(PAD <= 4 && 4 - PAD + KS - 1 + C1_T - 1 < C1_W, "window t0-4 .. t0+7");
   constexpr int SH = 4 - PAD;  // window index of tap 0 for output t0
@@ -171,11 +171,7 @@ __global__ __launch_bounds__(256) void conv_cout1_stream_kernel(ConvArgs a) {
       }
     };
     auto accum = [&](int c, float (&xv)[C1_W]) {
-      if constexpr (SNAKE) {
-        const float al = a.alpha[c], ia = a.inv_alpha[c];
-#pragma unroll
-        for (int j = 0; j < C1_W; ++j) xv[j] = snake_act(xv[j], al, ia);  // snake(0) = 0
-      }
+      if constexpr (SNAKE) snake_n1<C1_W>(xv, a.alpha[c], a.inv_alpha[c]);  // snake(0) = 0
 #pragma unroll
       for (int k = 0; k < KS; ++k) {
         const float wv = a.w[(size_t)(c * KS + k) * a.m_pad];
@@ -201,9 +197,9 @@ __global__ __launch_bounds__(256) void conv_cout1_stream_kernel(ConvArgs a) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   if (interior) {
-    if (a.alpha) run(T_{}, T_{}); else run(T_{}, F_{});
+    run(T_{}, std::integral_constant<bool, SNK>{});
   } else {
-    if (a.alpha) run(F_{}, T_{}); else run(F_{}, F_{});
+    run(F_{}, std::integral_constant<bool, SNK>{});
   }
 #pragma unroll
   for (int u = 0; u < C1_T; ++u) {
@@ -225,10 +221,16 @@ int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
       ((ks == 7 && a.pad == 3) || (ks == 3 && a.pad == 1))) {
     const long long nblk = (long long)batch * ((a.ng + 256 * C1_T - 1) / (256 * C1_T));
     if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-    if (ks == 7)
-      hipLaunchKernelGGL((conv_cout1_stream_kernel<7, 3>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+    // the consumer-side Snake variant is its own kernel: its registers do not set the plain
+    // variant's occupancy
+    if (ks == 7 && a.alpha)
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<7, 3, true>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+    else if (ks == 7)
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<7, 3, false>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+    else if (a.alpha)
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<3, 1, true>), dim3((unsigned)nblk), dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_cout1_stream_kernel<3, 1>), dim3((unsigned)nblk), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_cout1_stream_kernel<3, 1, false>), dim3((unsigned)nblk), dim3(256), 0, st, a);
     return vrvq_launch_status();
   }
   if (a.cin * ks * (a.M == 1 ? 1 : SMALL_COUT) > SMALL_WMAX) return VRVQ_ERR_UNSUPPORTED;

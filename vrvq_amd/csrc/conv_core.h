@@ -296,8 +296,7 @@ __device__ __forceinline__ void conv_epilogue(
   // in a rolled loop.
   float* ct = smem;
   const int mrows = min(BM, a.M - m0);
-#pragma unroll
-  for (int pass = 0; pass < EPASS; ++pass) {
+  for (int pass = 0; pass < EPASS; ++pass) {  // (unrolled by the compiler where it fits)
     if (pass > 0) __syncthreads();
     if (wn / (WN / EPASS) == pass) {
       const int cbase = wn * TN - pass * BNP;
@@ -370,8 +369,8 @@ __device__ __forceinline__ void conv_epilogue(
         if (a.ys) {
           for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
-            float sv[4];
-            for (int q = 0; q < 4; ++q) sv[q] = snake_act(v[u][q], sa[u], si[u]);
+            float sv[4] = {v[u][0], v[u][1], v[u][2], v[u][3]};
+            snake_n1<4>(sv, sa[u], si[u]);
             if (full[u]) {
               *reinterpret_cast<float4*>(a.ys + ob[u]) = make_float4(sv[0], sv[1], sv[2], sv[3]);
             } else {
@@ -424,12 +423,8 @@ __device__ __forceinline__ void conv_epilogue(
           }
           const size_t o = ((size_t)b * a.cout + co) * a.ylen + t0;
           const bool full = p0 + (tl0 + 3) / UP < a.ng && t0 >= 0 && t0 + 3 < a.ylen;
-          float sv[4];
-          if (a.ys) {
-            const float al = a.alpha_o[co], ia = a.inv_alpha_o[co];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) sv[u] = snake_act(v[u], al, ia);
-          }
+          float sv[4] = {v[0], v[1], v[2], v[3]};
+          if (a.ys) snake_n1<4>(sv, a.alpha_o[co], a.inv_alpha_o[co]);
           if (full) {
             typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
             if (a.y) *reinterpret_cast<f4u*>(a.y + o) = f4u{v[0], v[1], v[2], v[3]};

@@ -95,8 +95,10 @@ void ru_fused_kernel(RuArgs ra) {
           for (int j = 0; j < RN; ++j) {
             float v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-              v[u] = row0 + u < C ? snake_act(acc[i][j][4 * g + u] + bb[u], al[u], ia[u]) : 0.0f;
+            for (int u = 0; u < 4; ++u) v[u] = acc[i][j][4 * g + u] + bb[u];
+            snake_n<4>(v, al, ia);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = row0 + u < C ? v[u] : 0.0f;
             unsigned h[2], m[2], l[2];
             split3x2(v[0], v[1], h[0], m[0], l[0]);
             split3x2(v[2], v[3], h[1], m[1], l[1]);

@@ -184,11 +184,14 @@ __device__ __forceinline__ void conv_mainloop_x3(
         v[u] = ok ? xr[it][u] : 0.0f;
       }
       if (a.alpha != nullptr) {
+        float al[8], ia[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int ci = PH ? min(ci0 + c8 * 8 + u, a.cin - 1) >> psh : min(ci0 + c8 * 8 + u, a.cin - 1);
-          v[u] = snake_act(v[u], a.alpha[ci], a.inv_alpha[ci]);  // snake(0) = 0
+          al[u] = a.alpha[ci];
+          ia[u] = a.inv_alpha[ci];
         }
+        snake_n<8>(v, al, ia);  // snake(0) = 0
       }
       unsigned h[4], m[4], l[4];
 #pragma unroll
@@ -284,7 +287,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
   }
 }
 
-// LDS bytes the x3 mainloop needs for a window of XW positions.
+// LDS bytes the x3 mainloop needs for a window of XW positions.// LDS bytes the x3 mainloop needs for a window of XW positions.
 template <int KS, int BM, int BN>
 inline size_t x3_lds_bytes(int xw) {
   return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM>() + 3 * (size_t)X3Cfg<KS>::NC8 * x3_xwp(xw) * 16);

@@ -675,12 +675,10 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
   const int n_tc = (frames + PJ_TC - 1) / PJ_TC;
   const dim3 grid((unsigned)(batch * n_tc), PJ_SPLIT, (unsigned)((nq + 7) / 8));
   const int lds = PJ_NC * PJ_STG * (int)sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
+  if (lds > 64 * 1024) {  // the attribute is per device: set on every launch that needs it
     hipError_t e = hipFuncSetAttribute((const void*)rvq_project_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return (int)e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(rvq_project_kernel, grid, dim3(PJ_NT), lds, st, z, frames, nq, n_tc, w_in_t,
                      part, (int)nf);
