@@ -203,6 +203,13 @@ int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_
 int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
                   vrvq_stream_t stream);
 
+/* Projection kernel used by vrvq_rvq_project / vrvq_rvq_encode (process-wide): 2 = one
+ * workgroup per clip x channel split, z slab staged once in LDS (default); 1 = 48-frame tiles x
+ * 64-row blocks. Both write the same partials bit for bit (A/B timing, bit-identity test; also
+ * VRVQ_RVQ_PROJECT=1 in the environment). variant 0 queries. Returns the previous variant (1 or
+ * 2), or VRVQ_ERR_ARG. */
+int vrvq_rvq_project_variant(int variant);
+
 /* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows). */
 int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
 

@@ -592,6 +592,30 @@ def test_rvq_encode_vs_fp64(nq, ncode, B, T, vbr):
     assert torch.equal(vrvq_amd.masked_sum(zqis, mask), zq)
 
 
+@pytest.mark.parametrize("nq,B,T", [(8, 32, 87), (32, 64, 87), (28, 3, 70), (1, 4, 87), (5, 3, 40),
+                                    (9, 2, 200), (2, 1, 1), (12, 2, 97)])
+def test_rvq_projection_variants_bit_identical(nq, B, T):
+    """The clip x split projection kernel (default) and the 48-frame-tile kernel write the same
+    partials: every output of rvq_encode is bit-identical between them (odd nq, partial frame
+    tiles, T > 96, one frame, full config-2/3 batches)."""
+    from vrvq_amd import _lib
+    q, gen = _random_rvq(nq, 1024, 31 * nq + T)
+    st = q.stacked()
+    z = (torch.randn(B, 1024, T, generator=gen) * 0.3).to(DEV)
+    imp = torch.rand(B, T, generator=gen).to(DEV)
+    outs = {}
+    prev = _lib.rvq_project_variant(0)
+    try:
+        for v in (1, 2):
+            _lib.rvq_project_variant(v)
+            outs[v] = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=0.8)
+            torch.cuda.synchronize()
+    finally:
+        _lib.rvq_project_variant(prev)
+    for a, b in zip(outs[1], outs[2]):
+        assert (a is None and b is None) or torch.equal(a, b)
+
+
 def test_rvq_big_batch_nq32_properties():
     """BASELINE config 3 shape (B=64, 32 codebooks) on random weights: fp64 codes agreement
     and the invariants at full size."""

@@ -7,7 +7,7 @@ P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIV
 P2="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"
 P3="FETCH_SIZE"
 P4="WRITE_SIZE"
-for K in project chain expand; do
+for K in ${KERNELS:-project chain expand}; do
   j=0
   for P in "$P1" "$P2" "$P3" "$P4"; do
     j=$((j+1))

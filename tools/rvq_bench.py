@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
+    ap.add_argument("--variants", default="2", help="projection kernel variants to time (1,2)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -37,22 +38,25 @@ def main():
     z = (torch.randn(args.batch, 1024, args.frames, generator=g) * 0.3).to(dev)
     imp = torch.rand(args.batch, args.frames, generator=g).to(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ts = []
     run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
                                  want_z_q_is=not args.no_zqis)
-    for it in range(args.iters):
-        e0.record()
-        run()
-        e1.record()
-        torch.cuda.synchronize()
-        if it >= min(5, args.iters - 1):
-            ts.append(e0.elapsed_time(e1) * 1e3)
-    med = sorted(ts)[len(ts) // 2]
-    byt = rvq_bytes(args.batch, args.frames, args.nq)
-    tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
-    print(f"B={args.batch} nq={args.nq} T={args.frames}: {tag} median {med:.1f} us "
-          f"(min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
-          f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB")
+    from vrvq_amd import _lib
+    for v in [int(x) for x in args.variants.split(",")]:
+        _lib.rvq_project_variant(v)
+        ts = []
+        for it in range(args.iters):
+            e0.record()
+            run()
+            e1.record()
+            torch.cuda.synchronize()
+            if it >= min(5, args.iters - 1):
+                ts.append(e0.elapsed_time(e1) * 1e3)
+        med = sorted(ts)[len(ts) // 2]
+        byt = rvq_bytes(args.batch, args.frames, args.nq)
+        tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
+        print(f"projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
+              f"{med:.1f} us (min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
+              f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB")
 
 
 if __name__ == "__main__":

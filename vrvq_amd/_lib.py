@@ -71,7 +71,8 @@ SIGNATURES = {
     "vrvq_rvq_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P,
                           _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
 }
-EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)}
+EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
+         "vrvq_rvq_project_variant": ([_I], _I)}
 
 _lock = threading.Lock()
 _lib = None
@@ -109,3 +110,12 @@ def call(name: str, *args) -> None:
     if rc != 0:
         msg = lib.vrvq_status_string(rc)
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else 'unknown'}")
+
+
+def rvq_project_variant(variant: int = 0) -> int:
+    """Select the RVQ projection kernel (2: clip x split workgroups, default; 1: 48-frame tiles;
+    0: query). Returns the previous variant. Both write the same bits (tests/test_gpu_parity.py)."""
+    prev = load().vrvq_rvq_project_variant(variant)
+    if prev not in (1, 2):
+        raise RuntimeError(f"vrvq_rvq_project_variant({variant}) failed ({prev})")
+    return prev

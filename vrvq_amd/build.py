@@ -54,12 +54,12 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build vrvq_amd)")
 
 
-def _compile_and_link(out: str, extra, verbose: bool, tag: str) -> str:
+def _compile_and_link(out: str, extra, verbose: bool, tag: str, srcs=None) -> str:
     """One hipcc process per translation unit (they compile in parallel), then one link."""
     os.makedirs(OBJ_DIR, exist_ok=True)
     procs, objs = [], []
     headers = [d for d in deps() if not d.endswith(".hip")]
-    for src in sources():
+    for src in (srcs or sources()):
         obj = os.path.join(OBJ_DIR, os.path.basename(src)[:-4] + tag + ".o")
         objs.append(obj)
         if os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj)
@@ -113,9 +113,10 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
 
 
 def build_stamped(verbose: bool = True) -> str:
-    """Diagnostic build with in-kernel s_memtime stamps (tools/rvq_stamps.py)."""
+    """Diagnostic build with in-kernel s_memtime stamps (tools/rvq_chain_stamps.py): the RVQ
+    translation unit only (the stamped kernels and the entry points the tool calls)."""
     return _compile_and_link(os.path.join(HERE, "libvrvq_hip_stamps.so"), ["-DVRVQ_STAMPS"],
-                             verbose, "_stamps")
+                             verbose, "_stamps", srcs=[os.path.join(CSRC, "rvq.hip")])
 
 
 if __name__ == "__main__":

@@ -210,6 +210,109 @@ __global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------
+// Projection, one workgroup per (clip, frame tile of <= 96, channel split): the same partials,
+// bit for bit, as rvq_project_kernel (each wave runs that kernel's MFMA sequence: the split's
+// 128 channels in order, 4 per v_mfma_f32_16x16x4_f32, from a zero accumulator), reorganised so
+// that a workgroup reads its z slab [128 ch][<= 96 t] from HBM once (row segments, staged in
+// LDS in four 32-channel chunks, each consumed as soon as it has landed) and keeps it for every
+// 64-row block of stages; the w_in_t operands go straight to registers (32 per lane and block).
+// 8 waves: wave w = 16-row tile (w & 3) x three 16-frame column tiles (w >> 2). 256 workgroups
+// at configs[1] (32 clips x 8 splits): one per CU, no second round.
+constexpr int PJ2_NT = 512;
+constexpr int PJ2_TC = 96;                      // frames per tile (6 MFMA column tiles)
+constexpr int PJ2_LD = 112;                     // z_s row stride (112 = 48 mod 64: lk groups
+                                                // of the B reads land on disjoint bank ranges)
+constexpr int PJ2_ZQ = PJ_KC * PJ2_TC / PJ2_NT; // z loads per thread per K chunk (6)
+
+__global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __restrict__ z, int T,
+                                                              int nq, int n_tc,
+                                                              const float* __restrict__ w_in_t,
+                                                              float* __restrict__ part, int NF) {
+  __shared__ __attribute__((aligned(16))) float z_s[PJ_CPS * PJ2_LD];
+  const int tc = blockIdx.x % n_tc, b = blockIdx.x / n_tc;
+  const int s = blockIdx.y;
+  const int R = nq * RCD;
+  const int t0 = tc * PJ2_TC;
+  const int ntl = min(PJ2_TC, T - t0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int rt = wave & 3, ch = wave >> 2;  // row tile, column-tile half
+  // A operands of row block rb: row r = 64 rb + 16 rt + lr (stage r / 8, k = r % 8), channels
+  // 4 j + lk of the split; rows >= R zeroed (clamped address, mask)
+  auto load_w = [&](int rb, float (&av)[PJ_CPS / 4]) {
+    const int r = rb * 64 + rt * 16 + lr;
+    const unsigned m = 0u - (unsigned)(r < R);
+    const float* wp = w_in_t + ((size_t)min(r >> 3, nq - 1) * RD + s * PJ_CPS + lk) * RCD + (r & 7);
+#pragma unroll
+    for (int j = 0; j < PJ_CPS / 4; ++j)
+      av[j] = __uint_as_float(__float_as_uint(wp[(size_t)4 * j * RCD]) & m);
+  };
+  float av[PJ_CPS / 4];
+  load_w(0, av);  // L2-resident weights first, their latency under the z slab's
+  const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
+  {  // the slab: every load in flight at once
+    float zv[PJ_NC][PJ2_ZQ];
+#pragma unroll
+    for (int kc = 0; kc < PJ_NC; ++kc)
+#pragma unroll
+      for (int q = 0; q < PJ2_ZQ; ++q) {
+        const int e = tid + PJ2_NT * q;
+        const int c = e / PJ2_TC, t = e - c * PJ2_TC;
+        zv[kc][q] = zb[(size_t)(kc * PJ_KC + c) * T + min(t, ntl - 1)];  // clamped, zeroed below
+      }
+    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first wait
+#pragma unroll
+    for (int kc = 0; kc < PJ_NC; ++kc)
+#pragma unroll
+      for (int q = 0; q < PJ2_ZQ; ++q) {
+        const int e = tid + PJ2_NT * q;
+        const int c = e / PJ2_TC, t = e - c * PJ2_TC;
+        z_s[(kc * PJ_KC + c) * PJ2_LD + t] =
+            __uint_as_float(__float_as_uint(zv[kc][q]) & (0u - (unsigned)(t < ntl)));
+      }
+  }
+  // a use of the weights here keeps their loads ahead of the slab's (issued first, they have
+  // landed by now); without it they are sunk below the barrier and waited for one by one
+#pragma unroll
+  for (int j = 0; j < PJ_CPS / 4; ++j) asm volatile("" ::"v"(av[j]));
+  __syncthreads();
+  for (int rb = 0; rb * 64 < R; ++rb) {
+    float an[PJ_CPS / 4];
+    const bool more = (rb + 1) * 64 < R;
+    if (more) load_w(rb + 1, an);  // next block's weights under this block's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < PJ_CPS / 4; ++j) {
+      const float* zr = z_s + (4 * j + lk) * PJ2_LD + ch * 48 + lr;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], zr[q * 16], acc[q], 0, 0, 0);
+    }
+    // D layout: lane l, reg q -> row 4 (l >> 4) + q of the tile, frame l & 15
+    const int rr = rb * 64 + rt * 16 + 4 * lk;  // rows rr..rr+3 all valid iff rr < R
+    if (rr < R) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int t = ch * 48 + q * 16 + lr;
+        if (t < ntl) {
+          const size_t n = (size_t)b * T + t0 + t;
+          *reinterpret_cast<float4*>(part + ((size_t)s * NF + n) * R + rr) =
+              make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < PJ_CPS / 4; ++j) av[j] = an[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // The chain. Workgroup = frames [n0, n0 + nf) of the flattened (b, t) axis, nf <= 16; 8 waves.
 //
 // Stage i, S1 (all waves):
@@ -668,10 +771,30 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Projection kernel: 2 = rvq_project2_kernel (one workgroup per clip x split, default), 1 =
+// rvq_project_kernel (48-frame tiles x 64-row blocks). Same partials bit for bit (A/B timing and
+// the bit-identity test; VRVQ_RVQ_PROJECT=1 in the environment).
+int g_project_variant = 0;  // 0: not yet read from the environment
+
+int project_variant() {
+  if (g_project_variant == 0) {
+    const char* e = getenv("VRVQ_RVQ_PROJECT");
+    g_project_variant = (e && e[0] == '1') ? 1 : 2;
+  }
+  return g_project_variant;
+}
+
 int launch_project(const float* z, int batch, int frames, int nq, const float* w_in_t,
                    float* part, hipStream_t st) {
   const long long nf = (long long)batch * frames;
   VRVQ_CHECK_ARG(nf * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
+  if (project_variant() == 2) {
+    const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
+    VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
+    hipLaunchKernelGGL(rvq_project2_kernel, dim3((unsigned)(batch * n_tc), PJ_SPLIT), dim3(PJ2_NT),
+                       0, st, z, frames, nq, n_tc, w_in_t, part, (int)nf);
+    return vrvq_launch_status();
+  }
   const int n_tc = (frames + PJ_TC - 1) / PJ_TC;
   const dim3 grid((unsigned)(batch * n_tc), PJ_SPLIT, (unsigned)((nq + 7) / 8));
   const int lds = PJ_NC * PJ_STG * (int)sizeof(float);
@@ -749,6 +872,13 @@ extern "C" int vrvq_debug_set_stamps(unsigned long long* buf) {
   return 0;
 }
 #endif
+
+extern "C" int vrvq_rvq_project_variant(int variant) {
+  const int prev = project_variant();
+  if (variant == 1 || variant == 2) g_project_variant = variant;
+  else if (variant != 0) return VRVQ_ERR_ARG;
+  return prev;
+}
 
 extern "C" int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_out,
                                    int nq, int dim, int cdim, float* mcol, float* qb,
