@@ -112,6 +112,28 @@ def test_snake_conv_grads_vs_torch64(case):
         assert l2rel(resd.grad.cpu().numpy(), res64.grad.numpy()) < TOL
 
 
+@pytest.mark.parametrize("cin,cout,k,pad,dil,T,snake", [
+    (64, 96, 7, 9, 3, 700, True), (96, 96, 1, 0, 1, 257, True), (1024, 1024, 3, 1, 1, 87, True),
+    (192, 192, 7, 27, 9, 300, False), (33, 70, 7, 3, 1, 65, True), (8, 1, 3, 1, 1, 40, True)])
+def test_wgrad_x3_vs_torch64(cin, cout, k, pad, dil, T, snake):
+    """Stride-1 weight gradients run on the split bf16 MFMA (wgrad_x3_kernel): against a torch
+    fp64 conv1d_weight within 1e-5 (l2 rel), and within 4x the fp32 error bound, for partial
+    tiles, every tap-group size, dilations 1/3/9 and a Snake on the layer input."""
+    g0 = torch.Generator().manual_seed(cin + k)
+    a = torch.randn(2, cout, T, generator=g0)
+    x = torch.randn(2, cin, T, generator=g0)
+    alpha = torch.rand(cin, generator=g0) + 0.5
+    snk = None
+    xs64 = x.double()
+    if snake:
+        al = alpha.to(DEV)
+        snk = (al, 1.0 / (al + 1e-9))
+        xs64 = snake64(x.double(), alpha.double()[None, :, None])
+    r = ops.conv1d_wgrad(a.to(DEV), x.to(DEV), k, 1, pad, dil, snake_x=snk)
+    ref = torch.nn.grad.conv1d_weight(xs64, (cout, cin, k), a.double(), 1, pad, dil)
+    assert l2rel(r.cpu().numpy(), ref.numpy()) < 1e-5
+
+
 def test_wgrad_deterministic():
     g0 = torch.Generator().manual_seed(3)
     a = torch.randn(3, 96, 700, generator=g0).to(DEV)

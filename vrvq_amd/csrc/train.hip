@@ -7,8 +7,7 @@
 //   ConvTranspose1d (k = 2s):        dXs = conv1d(dY, W, stride s, pad)
 // Every reduction is deterministic (fixed order; split-K partials summed in split order).
 #include "common.h"
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+#include "conv_x3.h"  // split3x2 / mfma_bf16: the x3 (split bf16) products of the forward convs
 
 namespace {
 
@@ -140,6 +139,139 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int c = c0 + wn * 32 + (lane & 31);
+      if (m < a.M && c < a.C && k0 + kk < a.K)
+        a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k0 + kk] = acc[kk][r];
+    }
+}
+
+// Weight gradient of the stride-1 convs on the split bf16 MFMA (the forward convs' "x3"
+// products, conv_x3.h): both operands split exactly into three bf16 terms, six
+// v_mfma_f32_32x32x16_bf16 per 16 time samples (m m, h l, l h, h m, m h, then h h), fp32
+// accumulation -- fp32-accurate (dropped terms <= 2^-23 |ab|) at 2.7x the fp32 MFMA ceiling.
+// Same workgroup geometry and split-K order as wgrad_kernel: (64 m x 64 c tile, KG taps, split),
+// 64-sample time chunks. A rows are staged pre-split ([3 planes][64][72] bf16, 16-byte rows);
+// the X window stays fp32 in LDS and each tap's shifted B operand (8 consecutive samples, any
+// alignment) is split in registers right before its MFMAs.
+constexpr int WX_KT = 64;
+constexpr int WX_ALD = WX_KT + 8;  // bf16 per A-plane row (144 B)
+
+template <int KG>
+__global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradArgs a) {
+  using namespace vrvq_conv;
+  extern __shared__ float wsm[];
+  unsigned* A3 = reinterpret_cast<unsigned*>(wsm);       // [3][64][WX_ALD / 2] bf16 pairs
+  float* X_s = wsm + 3 * 64 * WX_ALD / 2;                // [64][WP]
+  const int n_mt = (a.M + WG_BM - 1) / WG_BM, n_ct = (a.C + WG_BN - 1) / WG_BN;
+  int bid = blockIdx.x;
+  const int mt = bid % n_mt; bid /= n_mt;
+  const int ct = bid % n_ct; bid /= n_ct;
+  const int kg = bid % a.n_kg;
+  const int sp = bid / a.n_kg;
+  const int m0 = mt * WG_BM, c0 = ct * WG_BN, k0 = kg * KG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nct = (a.TA + WX_KT - 1) / WX_KT;
+  const int q0 = (int)((long long)sp * a.chunks / a.n_split);
+  const int q1 = (int)((long long)(sp + 1) * a.chunks / a.n_split);
+  constexpr int NU = WG_WMAX / 64;
+  // staging in two halves (32 A rows as pairs, 32 X-window rows), every load of a half before
+  // its stores, snake and the bf16 split between them
+  auto stage = [&](int q) {
+    const int b = q / nct, t0 = (q - b * nct) * WX_KT;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float av[4][2], xv[8][NU];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = tid + 256 * i, r = 32 * h + (e >> 5), j = (e & 31) * 2;
+        const int m = m0 + r;
+        const float* ap = a.A + ((size_t)b * a.M + min(m, a.M - 1)) * a.TA;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = t0 + j + u;
+          av[i][u] = (m < a.M && t < a.TA) ? ap[min(t, a.TA - 1)] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int c = c0 + wave + 4 * (8 * h + rr);
+        const float* xr = a.X + ((size_t)b * a.C + (c < a.C ? c : 0)) * a.TX;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int pp = lane + 64 * u, tx = t0 - a.p + k0 * a.d + pp;
+          xv[rr][u] = (pp < a.W && c < a.C && tx >= 0 && tx < a.TX) ? xr[tx] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = tid + 256 * i, r = 32 * h + (e >> 5), j = (e & 31) * 2;
+        float v0 = av[i][0], v1 = av[i][1];
+        if (a.alpha_a && m0 + r < a.M) {
+          v0 = snake_act(v0, a.alpha_a[m0 + r], a.inv_alpha_a[m0 + r]);
+          v1 = snake_act(v1, a.alpha_a[m0 + r], a.inv_alpha_a[m0 + r]);
+        }
+        unsigned hh, mm, ll;
+        split3x2(v0, v1, hh, mm, ll);
+        const int o = r * (WX_ALD / 2) + j / 2;
+        A3[o] = hh;
+        A3[64 * (WX_ALD / 2) + o] = mm;
+        A3[2 * 64 * (WX_ALD / 2) + o] = ll;
+      }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = wave + 4 * (8 * h + rr), c = c0 + r;
+        const bool sn = a.alpha && c < a.C;
+        const float cl = sn ? a.alpha[c] : 0.0f, icl = sn ? a.inv_alpha[c] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int pp = lane + 64 * u;
+          if (pp < a.W) X_s[r * a.WP + pp] = sn ? snake_act(xv[rr][u], cl, icl) : xv[rr][u];
+        }
+      }
+    }
+  };
+  f32x16 acc[KG];
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[kk][r] = 0.0f;
+  const u32x4* arow = reinterpret_cast<const u32x4*>(A3 + (wm * 32 + lr) * (WX_ALD / 2)) + lh;
+  const float* xrow = X_s + (wn * 32 + lr) * a.WP + 8 * lh;
+  for (int q = q0; q < q1; ++q) {
+    stage(q);
+    __syncthreads();
+    // 32x32x16 bf16: lane l holds A[m = l & 31][k = 8 (l >> 5) .. +7] and B[k][c = l & 31]
+#pragma unroll 1
+    for (int tp = 0; tp < WX_KT; tp += 16) {
+      const u32x4 ah = arow[tp / 8], am = arow[64 * (WX_ALD / 8) + tp / 8],
+                  al = arow[2 * 64 * (WX_ALD / 8) + tp / 8];
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk) {
+        const float* xp = xrow + tp + kk * a.d;
+        unsigned bh[4], bm[4], bl[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) split3x2(xp[2 * u], xp[2 * u + 1], bh[u], bm[u], bl[u]);
+        const u32x4 h = {bh[0], bh[1], bh[2], bh[3]}, m = {bm[0], bm[1], bm[2], bm[3]},
+                    l = {bl[0], bl[1], bl[2], bl[3]};
+        f32x16 t = acc[kk];
+        t = mfma_bf16(am, m, t);  // m m
+        t = mfma_bf16(ah, l, t);  // h l
+        t = mfma_bf16(al, h, t);  // l h
+        t = mfma_bf16(ah, m, t);  // h m
+        t = mfma_bf16(am, h, t);  // m h
+        acc[kk] = mfma_bf16(ah, h, t);  // h h
+      }
+    }
+    __syncthreads();
+  }
+  // D: lane l, reg r -> row (r & 3) + 8 (r >> 2) + 4 (l >> 5), col l & 31
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int c = c0 + wn * 32 + lr;
       if (m < a.M && c < a.C && k0 + kk < a.K)
         a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k0 + kk] = acc[kk][r];
     }
@@ -300,13 +432,28 @@ extern "C" int vrvq_wgrad_plan(int batch, int m, int ta, int c, int k, int* n_sp
 }
 
 template <int KG>
-int launch_wgrad(WgradArgs w, hipStream_t st) {
+int launch_wgrad(WgradArgs w, hipStream_t st, bool x3) {
   const long long nblk = (long long)((w.M + WG_BM - 1) / WG_BM) * ((w.C + WG_BN - 1) / WG_BN) *
                          w.n_kg * w.n_split;
   if (nblk >= 0x7fffffffLL) return VRVQ_ERR_ARG;
+  if (x3) {
+    const size_t lds = (size_t)(3 * 64 * WX_ALD / 2 + 64 * w.WP) * sizeof(float);
+    hipLaunchKernelGGL(wgrad_x3_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
+    return vrvq_launch_status();
+  }
   const size_t lds = (size_t)(64 * ((1 << w.kt_sh) + 1) + 64 * w.WP) * sizeof(float);
   hipLaunchKernelGGL(wgrad_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
   return vrvq_launch_status();
+}
+
+// Stride-1 weight gradients on the split bf16 MFMA (wgrad_x3_kernel) unless VRVQ_WGRAD_X3=0
+// (A/B and tests: the fp32-input MFMA kernel for every shape).
+static bool wgrad_x3_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("VRVQ_WGRAD_X3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
@@ -328,18 +475,20 @@ extern "C" int vrvq_conv1d_wgrad(const float* a, int batch, int m, int ta,
     if (w.W <= WG_WMAX) break;
   }
   if (w.W > WG_WMAX) return VRVQ_ERR_UNSUPPORTED;
+  // the x3 kernel: stride 1, 64-sample chunks (window <= 64 + 7 * 9 samples)
+  const bool x3 = wgrad_x3_enabled() && stride == 1 && w.kt_sh == 6;
   w.WP = w.W | 1;
   w.chunks = batch * ((ta + (1 << w.kt_sh) - 1) >> w.kt_sh);
   if (w.n_split > w.chunks) w.n_split = w.chunks;
   hipStream_t st = as_stream(stream);
   int rc;
   switch (kg) {
-    case 1: rc = launch_wgrad<1>(w, st); break;
-    case 2: rc = launch_wgrad<2>(w, st); break;
-    case 3: rc = launch_wgrad<3>(w, st); break;
-    case 4: rc = launch_wgrad<4>(w, st); break;
-    case 7: rc = launch_wgrad<7>(w, st); break;
-    default: rc = launch_wgrad<8>(w, st); break;
+    case 1: rc = launch_wgrad<1>(w, st, x3); break;
+    case 2: rc = launch_wgrad<2>(w, st, x3); break;
+    case 3: rc = launch_wgrad<3>(w, st, x3); break;
+    case 4: rc = launch_wgrad<4>(w, st, x3); break;
+    case 7: rc = launch_wgrad<7>(w, st, x3); break;
+    default: rc = launch_wgrad<8>(w, st, x3); break;
   }
   if (rc) return rc;
   const size_t n_elem = (size_t)m * c * k;
