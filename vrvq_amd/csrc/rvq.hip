@@ -50,8 +50,9 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 // ------------------------------------------------------------------------------------------
 // Prep (once per weight version, like the weight-norm fold):
-//   mcol[j][i][k][m] = sum_c W_in(i)[k][c] W_out(j)[c][m] for i > j (else 0)
-//   qb[i][k]         = sum_c W_in(i)[k][c] (sum_{j<i} b_out(j)[c])   (bias sum in stage order)
+//   mcol[j][i][k][m] = sum_c W_in(i)[k][c] W_out(j)[c][m] for i > j (else 0)   (this kernel)
+//   qb[i][k]         = sum_c W_in(i)[k][c] (sum_{j<i} b_out(j)[c])   (cross_prep_qb_kernel)
+// one fmaf chain over c in order per output.
 __global__ void cross_prep_kernel(const float* __restrict__ w_in_t,  // [nq][D][8]
                                   const float* __restrict__ w_out,   // [nq][D][8]
                                   const float* __restrict__ b_out,   // [nq][D]
@@ -68,16 +69,28 @@ __global__ void cross_prep_kernel(const float* __restrict__ w_in_t,  // [nq][D][
       for (int c = 0; c < RD; ++c) acc = fmaf(wi[c * RCD], wo[c * RCD], acc);
     }
     mcol[e] = acc;
-  } else if (e < nm + nq * RCD) {
-    const int q = e - nm, i = q / RCD, k = q % RCD;
-    const float* wi = w_in_t + (size_t)i * RD * RCD + k;
+  }
+}
+
+// qb with the bias prefix sums shared: workgroup = stage i; thread c forms
+// bs[c] = sum_{j<i} b_out(j)[c] (left to right) into LDS, then 8 lanes run the k-th fmaf chain
+// over c in order -- the values of the earlier one-thread-per-output form, which re-summed the
+// biases for every channel in each of its nq * 8 threads (O(nq^2 D) serial work: ~1 ms per
+// weight version at nq = 28, i.e. every training step).
+__global__ __launch_bounds__(RD) void cross_prep_qb_kernel(const float* __restrict__ w_in_t,
+                                                           const float* __restrict__ b_out,
+                                                           float* __restrict__ qb) {
+  __shared__ float bs_s[RD];
+  const int i = blockIdx.x, c = threadIdx.x;
+  float bs = 0.0f;
+  for (int j = 0; j < i; ++j) bs = bs + b_out[(size_t)j * RD + c];
+  bs_s[c] = bs;
+  __syncthreads();
+  if (c < RCD) {
+    const float* wi = w_in_t + (size_t)i * RD * RCD + c;
     float acc = 0.0f;
-    for (int c = 0; c < RD; ++c) {
-      float bs = 0.0f;
-      for (int j = 0; j < i; ++j) bs = bs + b_out[(size_t)j * RD + c];
-      acc = fmaf(wi[c * RCD], bs, acc);
-    }
-    qb[q] = acc;
+    for (int cc = 0; cc < RD; ++cc) acc = fmaf(wi[cc * RCD], bs_s[cc], acc);
+    qb[i * RCD + c] = acc;
   }
 }
 
@@ -885,9 +898,12 @@ extern "C" int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, cons
                                    vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(w_in_t && w_out && b_out && mcol && qb && nq > 0);
   if (dim != RD || cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
-  const int total = nq * nq * 64 + nq * RCD;
+  // mcol: one thread per (j, i, k, m) chain; qb: one workgroup per stage (cross_prep_qb_kernel)
+  const int total = nq * nq * 64;
   hipLaunchKernelGGL(cross_prep_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      as_stream(stream), w_in_t, w_out, b_out, nq, mcol, qb);
+  hipLaunchKernelGGL(cross_prep_qb_kernel, dim3(nq), dim3(RD), 0, as_stream(stream), w_in_t, b_out,
+                     qb);
   return vrvq_launch_status();
 }
 
