@@ -48,7 +48,7 @@ X3_PEAK_TFLOPS = 2516.6 / 6    # fp32 FLOPs on the bf16 MFMA with the exact 3-wa
 CLIP_SAMPLES = 44100
 SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
-RVQ_KERNELS = ("rvq_project_kernel", "rvq_chain_kernel", "rvq_expand_kernel")
+RVQ_KERNELS = ("rvq_project2_kernel", "rvq_chain_kernel", "rvq_expand_kernel")
 
 
 def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024) -> int:
@@ -61,7 +61,10 @@ def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024)
 
 
 def newest(pattern: str):
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    """Newest (by round-tag name) configs[1] record; the configs[2]-shape records (*cfg3*) are
+    not this line's."""
+    files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", pattern))
+                   if "cfg3" not in os.path.basename(f))
     return files[-1] if files else None
 
 
@@ -444,7 +447,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "RVQ path: rvq_project_kernel -> rvq_chain_kernel -> "
+                         "kernel": "RVQ path: rvq_project2_kernel -> rvq_chain_kernel -> "
                                    "rvq_expand_kernel (one torch.ops.vrvq.rvq_encode)",
                          "bytes_per_launch": byt, "path_us": round(rvq_ms * 1e3, 2),
                          "kernel_us_rocprof": split, "kernel_us_source": split_src},

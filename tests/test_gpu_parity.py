@@ -67,6 +67,33 @@ def test_model_forward_vs_reference(manifest, name):
         np.testing.assert_array_equal(out["mask_imp"].cpu().numpy(), g["mask_imp"])
 
 
+def test_x3_error_over_the_whole_chain(manifest):
+    """The split-bf16 ("x3") convs over the ~60 chained layers of encoder + decoder: their end-
+    to-end error against the reference's own outputs stays at the fp32-input MFMA path's level
+    (z, latents and audio within 4x that path's error and within 2e-5), and codes agree."""
+    g = load_golden("golden_nq8")
+    name = "golden_nq8"
+    m = manifest[name]
+    errs = {}
+    prev = ops.X3
+    try:
+        for x3 in (False, True):
+            ops.X3 = x3
+            model = vrvq_amd.DAC_VRVQ(**m["kwargs"])
+            load_recipe(model, m["weight_seed"])
+            model = model.to(DEV).eval()
+            with torch.no_grad():
+                out = model(t(g["audio_in"]), 44100, m["n_quantizers"], 1)
+            np.testing.assert_array_equal(out["codes"].cpu().numpy(), g["codes"])
+            errs[x3] = {k: rel_err(out[k].cpu().numpy(), g[r])
+                        for k, r in (("z", "z_q"), ("latents", "latents"), ("audio", "audio_out"))}
+    finally:
+        ops.X3 = prev
+    for k in errs[True]:
+        assert errs[True][k] < 2e-5, (k, errs)
+        assert errs[True][k] <= 4 * max(errs[False][k], 1e-6), (k, errs)
+
+
 @pytest.mark.parametrize("name", ["golden_nq8", "golden_nq28"])
 def test_encoder_and_decoder_units(manifest, name):
     g = load_golden(name)
