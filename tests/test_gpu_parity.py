@@ -532,6 +532,24 @@ def test_deterministic(manifest):
         assert torch.equal(a[k], b[k]), k
 
 
+def test_batch_invariance_full_batch(manifest):
+    """Every clip of the configs[1] batch (B = 32) against the same clip run in small batches
+    (the oracle checks 8 of the 32 clips): codes and masks identical, latents / z_q / audio
+    within 1e-6 (the conv tile choice may depend on the batch), so no clip position of the full
+    batch is computed differently from the small-batch path the oracle pins."""
+    model = model_for(manifest, "golden_nq8")
+    audio = t(synthetic_audio(32, 44100, seed=2024))
+    with torch.no_grad():
+        full = model(audio, 44100, None, 1)
+        for part in (range(0, 4), range(4, 13), range(13, 32)):
+            idx = list(part)
+            sub = model(audio[idx].contiguous(), 44100, None, 1)
+            for k in ("codes", "mask_imp"):
+                assert torch.equal(full[k][idx], sub[k]), (k, idx[0])
+            for k in ("latents", "z", "audio"):
+                assert rel_err(full[k][idx].cpu().numpy(), sub[k].cpu().numpy()) < 1e-6, (k, idx[0])
+
+
 def test_cbr_mode_of_vbr_model(manifest):
     model = model_for(manifest, "golden_nq8")
     audio = t(synthetic_audio(1, 44100, seed=3))
