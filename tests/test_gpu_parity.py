@@ -336,6 +336,15 @@ def test_conv1d_x3_vs_torch(case):
     assert e3 <= 4 * e32 + 2e-7, (e3, e32)
 
 
+@pytest.mark.parametrize("case", [(1, 256, 256, 4500, 7, 1, 3, 1, True, True, 0),
+                                  (2, 384, 384, 4100, 7, 1, 27, 9, True, False, 0),
+                                  (1, 128, 320, 5000, 7, 1, 3, 1, False, True, 0)])
+def test_conv1d_x3_long_rows_vs_torch(case):
+    """k7 x3 convs over rows of >= 4096 samples with >= 256 output channels: the shapes that take
+    the wide x3 tiles (VRVQ_CONV_X3_WIDE), ragged last tile and rows not a multiple of 64."""
+    test_conv1d_x3_vs_torch(case)
+
+
 @pytest.mark.parametrize("case", [(2, 64, 128, 1000, 2, 1, True), (2, 128, 256, 401, 4, 2, True),
                                   (2, 256, 512, 100, 8, 4, False), (2, 512, 1024, 696, 8, 4, False),
                                   (1, 64, 128, 513, 2, 0, True), (1, 8, 16, 37, 4, 2, True),

@@ -293,7 +293,7 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   a.mt_slow = conv_mt_slow();
   if constexpr (NW == 4 && BM <= 192 && (KS == 1 || KS == 2 || KS == 3 || KS == 7)) {
     constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
-    size_t lx = x3_lds_bytes<KS, BM, BN>(XW);
+    size_t lx = x3_lds_bytes<KS, BM, BN>(XW, a.cin);
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
         x3_tile_ok(BM, BN, KS, a)) {
@@ -393,6 +393,21 @@ static long long conv_bn96_min() {
   return v;
 }
 
+// x3 k7 layers over long rows (M a multiple of 64 and >= 128, Cin a multiple of 16): 64 x 256
+// tiles on 16-channel "pair" K-chunks (conv_x3.h: no zero octet, 168 MFMAs per wave between
+// barriers). 384 x 384 k7 at T = 5568, B = 32: 2027 -> 755-796 us (0.43 -> 0.50 of the x3
+// ceiling), 256 x 256: 934 -> 781-785 us (profiles/r03_x3_pair_ab.txt).
+// 768 x 768 / 512 x 512 k7 at T = 696: 1125 -> 962 / 514 -> 407 us despite 72 of every 768
+// columns padded. Tuning override VRVQ_CONV_X3_WIDE=0 (128- / 192-row tiles, 8-channel
+// chunks) | 1 (pair tiles for T >= 4096) | 2 (pair tiles for T >= 640, default).
+static int conv_x3_wide() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_X3_WIDE");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -420,6 +435,12 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
   if (a.M <= 32) return launch_cfg<32, 128, 1, 4, KS>(a, batch, st);
+  if constexpr (KS == 7) {
+    const int wide = conv_x3_wide();
+    if (a.w3 != nullptr && a.stride == 1 && a.up == 0 && a.M >= 128 && a.M % 64 == 0 &&
+        a.cin % 16 == 0 && ((wide >= 1 && a.ng >= 4096) || (wide == 2 && a.ng >= 640)))
+      return launch_cfg<64, 256, 1, 4, KS>(a, batch, st);
+  }
   if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
   if (bn == 96) return launch_cfg<128, 96, 4, 4, KS>(a, batch, st);
   constexpr bool kWide = KS == 1 || KS == 2 || KS == 3 || KS == 7;  // register budget at 512 threads

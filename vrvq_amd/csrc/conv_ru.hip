@@ -257,7 +257,7 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   const long long nblk = (long long)a.n_nt * batch;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
   if constexpr (BM <= 192) {
-    size_t lx = x3_lds_bytes<7, BM, BN>(XW);
+    size_t lx = x3_lds_bytes<7, BM, BN>(XW, a.cin);
     if (lx < hsz) lx = hsz;
     if (ru_p2x3<BM, BN>() && ra.w1x3 != nullptr && lx < (size_t)BM * BN * 6) lx = (size_t)BM * BN * 6;
     if (lx < epi) lx = epi;

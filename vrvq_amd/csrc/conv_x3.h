@@ -40,9 +40,18 @@ namespace vrvq_conv {
 template <int BM, int BN>
 constexpr int x3_stages() { return BM * BN <= 128 * 128 ? 1 : 2; }
 
-template <int KS>
-struct X3Cfg {
-  static constexpr int CK = KS == 1 ? 32 : KS <= 3 ? 16 : 8;  // channels per K-chunk
+// 64 x 256 k7 tiles ("pair" chunks): a K-chunk of 16 channels, two channel octets per tap, so
+// the 7 taps fill 14 octet slots = 7 MFMA steps with no zero octet (an 8-channel k7 chunk pads
+// its 7 octets to 8: 1/8 of its MFMAs multiply zero weights), 168 MFMAs per wave between two
+// barriers instead of 96. The weight planes stay in the 8-channel packing (two packed chunks
+// per K-chunk, pad octets skipped while staging): 43 KB W + <= 30 KB x per stage, two
+// workgroups per CU.
+template <int KS, int BM, int BN>
+constexpr bool x3_pair() { return KS == 7 && BM == 64 && BN == 256; }
+
+template <int KS, bool PAIR = false>
+struct X3Cfg {  // PAIR = false: also the HBM packing of the weight planes (vrvq_pack_x3_weight)
+  static constexpr int CK = PAIR ? 16 : KS == 1 ? 32 : KS <= 3 ? 16 : 8;  // channels per K-chunk
   static constexpr int NC8 = CK / 8;                        // channel octets per tap
   static constexpr int NO = KS * NC8;                       // octets per chunk
   static constexpr int NO2 = (NO + 1) & ~1;                 // padded to MFMA steps
@@ -70,9 +79,9 @@ __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
 }
 
 // LDS bytes of one pipeline stage.
-template <int KS, int BM>
+template <int KS, int BM, int BN>
 __host__ __device__ constexpr int x3_stage_w_bytes() {
-  return 3 * X3Cfg<KS>::NO2 * BM * 16;
+  return x3_pair<KS, BM, BN>() ? 2 * 3 * KS * BM * 16 : 3 * X3Cfg<KS>::NO2 * BM * 16;
 }
 __host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
 
@@ -81,10 +90,10 @@ __host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
 // Plain global loads (not LDS-DMA): the compiler then places the wait for them right before
 // the ds_write after the chunk's MFMAs; with LDS-DMA in inline asm it cannot see the loads and
 // its conservative waits at the next global load exposed their whole latency every chunk.
-template <int KS, int BM, int NT>
+template <int KS, int BM, int BN, int NT>
 struct X3W {
-  static constexpr int TOTAL = 3 * X3Cfg<KS>::NO2 * BM;  // uint4 per stage
-  static constexpr int WQ = (TOTAL + NT - 1) / NT;         // per thread
+  static constexpr int TOTAL = x3_stage_w_bytes<KS, BM, BN>() / 16;  // uint4 per stage
+  static constexpr int WQ = (TOTAL + NT - 1) / NT;                   // per thread
 };
 
 // K loop of the implicit GEMM on the split operands. Same contract as conv_mainloop (acc zero
@@ -98,12 +107,14 @@ __device__ __forceinline__ void conv_mainloop_x3(
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
     int n0) {
   using TC = TileCfg<BM, BN, WM, NW>;
-  using XC = X3Cfg<KS>;
+  constexpr bool PAIR = x3_pair<KS, BM, BN>();
+  using XC = X3Cfg<KS, PAIR>;
+  constexpr int NO2P = X3Cfg<KS>::NO2;  // octet slots per packed (HBM) chunk
   constexpr int NT = TC::NT, RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
   constexpr int CK = XC::CK, NC8 = XC::NC8, NO = XC::NO, NO2 = XC::NO2, NSTEP = XC::NSTEP;
   constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
   constexpr int XI = (NC8 * XW_MAX + NT - 1) / NT;  // x items (octet, position) per thread
-  constexpr int WB = x3_stage_w_bytes<KS, BM>();
+  constexpr int WB = x3_stage_w_bytes<KS, BM, BN>();
 
   const int XW = (BN - 1) + (KS - 1) * a.dil + 1;
   const int XWP = x3_xwp(XW);
@@ -123,14 +134,22 @@ __device__ __forceinline__ void conv_mainloop_x3(
   char* sbase = reinterpret_cast<char*>(smem);
 
 
-  constexpr int WQ = X3W<KS, BM, NT>::WQ, WTOT = X3W<KS, BM, NT>::TOTAL;
+  constexpr int WQ = X3W<KS, BM, BN, NT>::WQ, WTOT = X3W<KS, BM, BN, NT>::TOTAL;
   u32x4 wr[WQ];
   auto load_w = [&](int chunk) {
 #pragma unroll
     for (int r = 0; r < WQ; ++r) {
       const int u = min(tid + r * NT, WTOT - 1);  // clamped: no conditional load
-      const int po = u / BM, row = u - po * BM;
-      wr[r] = w3[((size_t)chunk * 3 * NO2 + po) * a.m_pad + m0 + row];
+      if constexpr (PAIR) {
+        // stage entry ((half * 3 + plane) * KS + tap) * BM + row <- packed chunk 2 chunk + half
+        const int hp = u / (KS * BM), r2 = u - hp * (KS * BM);
+        const int tap = r2 / BM, row = r2 - tap * BM;
+        const int half = hp / 3, pl = hp - half * 3;
+        wr[r] = w3[(((size_t)(2 * chunk + half) * 3 + pl) * NO2P + tap) * a.m_pad + m0 + row];
+      } else {
+        const int po = u / BM, row = u - po * BM;
+        wr[r] = w3[((size_t)chunk * 3 * NO2 + po) * a.m_pad + m0 + row];
+      }
     }
   };
   auto store_w = [&](char* stg) {
@@ -144,11 +163,14 @@ __device__ __forceinline__ void conv_mainloop_x3(
   // / input runs in store_x, after the MFMAs. (A select here makes the wave wait for the
   // load before the chunk's MFMAs, and vmcnt retires in order, so that wait also covers the
   // W DMA issued before it: the whole memory latency exposed once per chunk.)
+  // pair tiles: every input channel's Snake parameters in LDS behind the stage (their 16 per
+  // chunk do not fit the scalar registers)
+  float* snl = reinterpret_cast<float*>(sbase + STG);
   auto load_x = [&](int ci0) {
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
       const int e = tid + it * NT;
-      const int c8 = e / XW, pos = e - c8 * XW;
+      const int c8 = NC8 == 1 ? 0 : e / XW, pos = e - c8 * XW;
       const int tc = min(max(xbase + pos, 0), a.tin - 1);
       const int cb = ci0 + (e < nitems ? c8 : 0) * 8;
 #pragma unroll
@@ -165,11 +187,27 @@ __device__ __forceinline__ void conv_mainloop_x3(
   };
   auto store_x = [&](char* stg, int ci0) {
     u32x4* xs = reinterpret_cast<u32x4*>(stg + WB);
+    // the chunk's channels are workgroup-uniform: their Snake parameters are loaded once per
+    // chunk outside the (divergent) item loop -- scalar loads, no vector-memory round trip
+    // between the chunk's barriers -- and selected per item by its channel octet
+    const bool sn = a.alpha != nullptr;
+    constexpr int NU = NC8 == 1 ? 8 : 1;
+    float alu[NU], iau[NU];
+    if constexpr (NC8 == 1) {
+      if (sn) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int ci = PH ? min(ci0 + u, a.cin - 1) >> psh : min(ci0 + u, a.cin - 1);
+          alu[u] = a.alpha[ci];
+          iau[u] = a.inv_alpha[ci];
+        }
+      }
+    }
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
       const int e = tid + it * NT;
       if (e >= nitems) continue;
-      const int c8 = e / XW, pos = e - c8 * XW;
+      const int c8 = NC8 == 1 ? 0 : e / XW, pos = e - c8 * XW;
       const int t = xbase + pos;
       const bool okp = t >= 0 && t < a.tin;
       float v[8];
@@ -183,13 +221,22 @@ __device__ __forceinline__ void conv_mainloop_x3(
         }
         v[u] = ok ? xr[it][u] : 0.0f;
       }
-      if (a.alpha != nullptr) {
+      if (sn) {
         float al[8], ia[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int ci = PH ? min(ci0 + c8 * 8 + u, a.cin - 1) >> psh : min(ci0 + c8 * 8 + u, a.cin - 1);
-          al[u] = a.alpha[ci];
-          ia[u] = a.inv_alpha[ci];
+          if constexpr (NC8 == 1) {
+            al[u] = alu[u];
+            ia[u] = iau[u];
+          } else if constexpr (PAIR) {  // from the LDS table (prologue)
+            const int ci = min(ci0 + c8 * 8 + u, a.cin - 1);
+            al[u] = snl[ci];
+            ia[u] = snl[a.cin + ci];
+          } else {
+            const int ci = PH ? min(ci0 + c8 * 8 + u, a.cin - 1) >> psh : min(ci0 + c8 * 8 + u, a.cin - 1);
+            al[u] = a.alpha[ci];
+            ia[u] = a.inv_alpha[ci];
+          }
         }
         snake_n<8>(v, al, ia);  // snake(0) = 0
       }
@@ -203,13 +250,69 @@ __device__ __forceinline__ void conv_mainloop_x3(
   };
 
   const int nchunks = (a.cin + CK - 1) / CK;
+  const int col = wn * TN + lr;
+  auto rd_at = [&](const u32x4* ws, const u32x4* xs, int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
+    // octet slot o = 2 q + lh: (tap, channel octet) in tap-major order; a pair chunk's slot
+    // (q, lh) is tap q of its packed chunk lh
+    const int o = 2 * q + lh;
+    const int tap = PAIR ? q : o < NO ? o / NC8 : 0;  // padded octet: zero weights, any valid x
+    const int c8 = PAIR ? lh : o - (o / NC8) * NC8;
+    const int wo = PAIR ? lh * 3 * KS + q : o;  // + plane * (PAIR ? KS : NO2)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+        av[p][i] = ws[(p * (PAIR ? KS : NO2) + wo) * BM + wm * TM + i * 32 + lr];
+    const int xo = c8 * XWP + col + tap * a.dil;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bv[p][j] = xs[p * NC8 * XWP + xo + j * 32];
+  };
+  auto mma_at = [&](const u32x4 (&av)[3][RM], const u32x4 (&bv)[3][RN]) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma_bf16(av[1][i], bv[1][j], t);  // m m
+        t = mfma_bf16(av[0][i], bv[2][j], t);  // h l
+        t = mfma_bf16(av[2][i], bv[0][j], t);  // l h
+        t = mfma_bf16(av[0][i], bv[1][j], t);  // h m
+        t = mfma_bf16(av[1][i], bv[0][j], t);  // m h
+        acc[i][j] = mfma_bf16(av[0][i], bv[0][j], t);  // h h
+      }
+  };
+  auto chunk_mma = [&](const u32x4* ws, const u32x4* xs) {
+    u32x4 a0[3][RM], b0[3][RN], a1[3][RM], b1[3][RN];
+    rd_at(ws, xs, 0, a0, b0);
+#pragma unroll
+    for (int q = 0; q < NSTEP; q += 2) {
+      if (q + 1 < NSTEP) rd_at(ws, xs, q + 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_at(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 2 < NSTEP) rd_at(ws, xs, q + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < NSTEP) mma_at(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if constexpr (PAIR) {
+    if (a.alpha != nullptr) {
+      for (int c = tid; c < a.cin; c += NT) {
+        snl[c] = a.alpha[c];
+        snl[a.cin + c] = a.inv_alpha[c];
+      }
+      __syncthreads();
+    }
+  }
   int cur = 0;
   load_w(0);
   load_x(0);
   store_w(sbase);
   store_x(sbase, 0);
   __syncthreads();
-  const int col = wn * TN + lr;
   for (int c = 0; c < nchunks; ++c) {
     // Next chunk's loads in flight during this chunk's MFMAs. Unconditional (the last chunk
     // reloads itself into the idle stage): under `if (more)` the compiler sinks the loads past
@@ -221,53 +324,8 @@ __device__ __forceinline__ void conv_mainloop_x3(
       load_x(cn * CK);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const u32x4* ws = reinterpret_cast<const u32x4*>(sbase + cur * STG);
-    const u32x4* xs = reinterpret_cast<const u32x4*>(sbase + cur * STG + WB);
-    auto rd = [&](int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
-      const int o = 2 * q + lh;
-      const int tap = o < NO ? o / NC8 : 0;  // padded octet: zero weights, any valid x
-      const int c8 = o - (o / NC8) * NC8;
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int i = 0; i < RM; ++i) av[p][i] = ws[(p * NO2 + o) * BM + wm * TM + i * 32 + lr];
-      const int xo = c8 * XWP + col + tap * a.dil;
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) bv[p][j] = xs[p * NC8 * XWP + xo + j * 32];
-    };
-    auto mma = [&](const u32x4 (&av)[3][RM], const u32x4 (&bv)[3][RN]) {
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          // small terms first, then h h (one accumulator: 64 fewer registers, so two
-          // workgroups fit per CU; the chunk's h h products still enter after its corrections)
-          f32x16 t = acc[i][j];
-          t = mfma_bf16(av[1][i], bv[1][j], t);  // m m
-          t = mfma_bf16(av[0][i], bv[2][j], t);  // h l
-          t = mfma_bf16(av[2][i], bv[0][j], t);  // l h
-          t = mfma_bf16(av[0][i], bv[1][j], t);  // h m
-          t = mfma_bf16(av[1][i], bv[0][j], t);  // m h
-          acc[i][j] = mfma_bf16(av[0][i], bv[0][j], t);  // h h
-        }
-    };
-    {
-      u32x4 a0[3][RM], b0[3][RN], a1[3][RM], b1[3][RN];
-      rd(0, a0, b0);
-#pragma unroll
-      for (int q = 0; q < NSTEP; q += 2) {
-        if (q + 1 < NSTEP) rd(q + 1, a1, b1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (q + 2 < NSTEP) rd(q + 2, a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (q + 1 < NSTEP) mma(a1, b1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
+    chunk_mma(reinterpret_cast<const u32x4*>(sbase + cur * STG),
+              reinterpret_cast<const u32x4*>(sbase + cur * STG + WB));
     if constexpr (X3_STAGES == 1) {
       // Single stage: the refill is not prefetched (its registers would coexist with the
       // MFMA operands and spill); the other workgroup on the CU runs its MFMAs meanwhile.
@@ -275,6 +333,9 @@ __device__ __forceinline__ void conv_mainloop_x3(
       if (c + 1 < nchunks) {
         load_w(cn);
         load_x(cn * CK);
+        // every load of the refill in flight before the first store waits on one (else the
+        // x loads are issued only after the W stores: two memory round trips per chunk)
+        __builtin_amdgcn_sched_barrier(0);
         store_w(nxt);
         store_x(nxt, cn * CK);
       }
@@ -287,10 +348,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
   }
 }
 
-// LDS bytes the x3 mainloop needs for a window of XW positions.// LDS bytes the x3 mainloop needs for a window of XW positions.
+// LDS bytes the x3 mainloop needs for a window of XW positions.
 template <int KS, int BM, int BN>
-inline size_t x3_lds_bytes(int xw) {
-  return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM>() + 3 * (size_t)X3Cfg<KS>::NC8 * x3_xwp(xw) * 16);
+inline size_t x3_lds_bytes(int xw, int cin) {
+  const size_t xb = 3 * (size_t)X3Cfg<KS, x3_pair<KS, BM, BN>()>::NC8 * x3_xwp(xw) * 16;
+  const size_t snake = x3_pair<KS, BM, BN>() ? 2 * (size_t)cin * sizeof(float) : 0;
+  return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM, BN>() + xb) + snake;
 }
 
 }  // namespace vrvq_conv

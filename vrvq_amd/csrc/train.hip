@@ -149,14 +149,171 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs a) {
 // v_mfma_f32_32x32x16_bf16 per 16 time samples (m m, h l, l h, h m, m h, then h h), fp32
 // accumulation -- fp32-accurate (dropped terms <= 2^-23 |ab|) at 2.7x the fp32 MFMA ceiling.
 // Same workgroup geometry and split-K order as wgrad_kernel: (64 m x 64 c tile, KG taps, split),
-// 64-sample time chunks. A rows are staged pre-split ([3 planes][64][72] bf16, 16-byte rows);
-// the X window stays fp32 in LDS and each tap's shifted B operand (8 consecutive samples, any
-// alignment) is split in registers right before its MFMAs.
+// 64-sample time chunks. Both operands are staged pre-split, once per chunk: A rows as
+// [3 planes][64][72] bf16 (16-byte rows), the X window as [3 planes][64][XPW] bf16 (odd dword
+// stride). A tap's B operand is 8 consecutive samples from an offset of any parity: 4 dwords per
+// plane when the tap shift k d is even, else 5 dwords re-aligned by 16 bits (v_alignbit) -- the
+// same bf16 planes the per-tap split in registers produced, for a fraction of the VALU.
 constexpr int WX_KT = 64;
 constexpr int WX_ALD = WX_KT + 8;  // bf16 per A-plane row (144 B)
 
+__host__ __device__ inline int wx_xpw(int w) {  // bf16 per X-plane row: >= w + 2, odd dwords
+  const int dw = (w + 3) / 2;
+  return 2 * (dw | 1);
+}
+
 template <int KG>
 __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(WgradArgs a) {
+  using namespace vrvq_conv;
+  extern __shared__ float wsm[];
+  unsigned* A3 = reinterpret_cast<unsigned*>(wsm);       // [3][64][WX_ALD / 2] bf16 pairs
+  unsigned* X3 = A3 + 3 * 64 * WX_ALD / 2;               // [3][64][XPW / 2] bf16 pairs
+  const int XD = wx_xpw(a.W) / 2;                         // dwords per X-plane row
+  const int n_mt = (a.M + WG_BM - 1) / WG_BM, n_ct = (a.C + WG_BN - 1) / WG_BN;
+  int bid = blockIdx.x;
+  const int mt = bid % n_mt; bid /= n_mt;
+  const int ct = bid % n_ct; bid /= n_ct;
+  const int kg = bid % a.n_kg;
+  const int sp = bid / a.n_kg;
+  const int m0 = mt * WG_BM, c0 = ct * WG_BN, k0 = kg * KG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nct = (a.TA + WX_KT - 1) / WX_KT;
+  const int q0 = (int)((long long)sp * a.chunks / a.n_split);
+  const int q1 = (int)((long long)(sp + 1) * a.chunks / a.n_split);
+  constexpr int NU2 = (WG_WMAX + 127) / 128;  // sample pairs per lane and X row
+  // staging in two halves (32 A rows, 32 X-window rows, both as sample pairs), every load of a
+  // half before its stores, snake and the bf16 split between them
+  auto stage = [&](int q) {
+    const int b = q / nct, t0 = (q - b * nct) * WX_KT;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float av[4][2], xv[8][NU2][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = tid + 256 * i, r = 32 * h + (e >> 5), j = (e & 31) * 2;
+        const int m = m0 + r;
+        const float* ap = a.A + ((size_t)b * a.M + min(m, a.M - 1)) * a.TA;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = t0 + j + u;
+          av[i][u] = (m < a.M && t < a.TA) ? ap[min(t, a.TA - 1)] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int c = c0 + wave + 4 * (8 * h + rr);
+        const float* xr = a.X + ((size_t)b * a.C + (c < a.C ? c : 0)) * a.TX;
+#pragma unroll
+        for (int u = 0; u < NU2; ++u)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const int pp = 2 * (lane + 64 * u) + v, tx = t0 - a.p + k0 * a.d + pp;
+            xv[rr][u][v] = (pp < a.W && c < a.C && tx >= 0 && tx < a.TX) ? xr[tx] : 0.0f;
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = tid + 256 * i, r = 32 * h + (e >> 5), j = (e & 31) * 2;
+        float v0 = av[i][0], v1 = av[i][1];
+        if (a.alpha_a && m0 + r < a.M) {
+          v0 = snake_act(v0, a.alpha_a[m0 + r], a.inv_alpha_a[m0 + r]);
+          v1 = snake_act(v1, a.alpha_a[m0 + r], a.inv_alpha_a[m0 + r]);
+        }
+        unsigned hh, mm, ll;
+        split3x2(v0, v1, hh, mm, ll);
+        const int o = r * (WX_ALD / 2) + j / 2;
+        A3[o] = hh;
+        A3[64 * (WX_ALD / 2) + o] = mm;
+        A3[2 * 64 * (WX_ALD / 2) + o] = ll;
+      }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = wave + 4 * (8 * h + rr), c = c0 + r;
+        const bool sn = a.alpha && c < a.C;
+        const float cl = sn ? a.alpha[c] : 0.0f, icl = sn ? a.inv_alpha[c] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NU2; ++u) {
+          const int pw = lane + 64 * u;  // pair index
+          if (2 * pw < a.W) {
+            float v0 = xv[rr][u][0], v1 = xv[rr][u][1];
+            if (sn) {
+              v0 = snake_act(v0, cl, icl);
+              v1 = snake_act(v1, cl, icl);
+            }
+            unsigned hh, mm, ll;
+            split3x2(v0, v1, hh, mm, ll);
+            X3[r * XD + pw] = hh;
+            X3[(64 + r) * XD + pw] = mm;
+            X3[(128 + r) * XD + pw] = ll;
+          }
+        }
+      }
+    }
+  };
+  f32x16 acc[KG];
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[kk][r] = 0.0f;
+  const u32x4* arow = reinterpret_cast<const u32x4*>(A3 + (wm * 32 + lr) * (WX_ALD / 2)) + lh;
+  const unsigned* xrow = X3 + (wn * 32 + lr) * XD + 4 * lh;  // sample 8 lh of row wn 32 + lr
+  for (int q = q0; q < q1; ++q) {
+    stage(q);
+    __syncthreads();
+    // 32x32x16 bf16: lane l holds A[m = l & 31][k = 8 (l >> 5) .. +7] and B[k][c = l & 31]
+#pragma unroll 1
+    for (int tp = 0; tp < WX_KT; tp += 16) {
+      const u32x4 ah = arow[tp / 8], am = arow[64 * (WX_ALD / 8) + tp / 8],
+                  al = arow[2 * 64 * (WX_ALD / 8) + tp / 8];
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk) {
+        const int sh = kk * a.d;                       // tap shift (wave-uniform)
+        const unsigned* xp = xrow + (tp + sh) / 2;
+        u32x4 bp[3];
+        if ((sh & 1) == 0) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const unsigned* r = xp + p * 64 * XD;
+            bp[p] = u32x4{r[0], r[1], r[2], r[3]};
+          }
+        } else {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const unsigned* r = xp + p * 64 * XD;
+            const unsigned d0 = r[0], d1 = r[1], d2 = r[2], d3 = r[3], d4 = r[4];
+            bp[p] = u32x4{__builtin_amdgcn_alignbit(d1, d0, 16), __builtin_amdgcn_alignbit(d2, d1, 16),
+                          __builtin_amdgcn_alignbit(d3, d2, 16), __builtin_amdgcn_alignbit(d4, d3, 16)};
+          }
+        }
+        f32x16 t = acc[kk];
+        t = mfma_bf16(am, bp[1], t);  // m m
+        t = mfma_bf16(ah, bp[2], t);  // h l
+        t = mfma_bf16(al, bp[0], t);  // l h
+        t = mfma_bf16(ah, bp[1], t);  // h m
+        t = mfma_bf16(am, bp[0], t);  // m h
+        acc[kk] = mfma_bf16(ah, bp[0], t);  // h h
+      }
+    }
+    __syncthreads();
+  }
+  // D: lane l, reg r -> row (r & 3) + 8 (r >> 2) + 4 (l >> 5), col l & 31
+#pragma unroll
+  for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int c = c0 + wn * 32 + lr;
+      if (m < a.M && c < a.C && k0 + kk < a.K)
+        a.part[(((size_t)sp * a.M + m) * a.C + c) * a.K + k0 + kk] = acc[kk][r];
+    }
+}
+
+// The 1x1 form (KG = 1): X staged fp32 and each 8-sample B operand split in registers -- with
+// one tap per staged window, splitting while staging buys nothing and costs a third LDS plane.
+template <int KG>
+__global__ __launch_bounds__(256, 2) void wgrad_x3_reg_kernel(WgradArgs a) {
   using namespace vrvq_conv;
   extern __shared__ float wsm[];
   unsigned* A3 = reinterpret_cast<unsigned*>(wsm);       // [3][64][WX_ALD / 2] bf16 pairs
@@ -437,8 +594,13 @@ int launch_wgrad(WgradArgs w, hipStream_t st, bool x3) {
                          w.n_kg * w.n_split;
   if (nblk >= 0x7fffffffLL) return VRVQ_ERR_ARG;
   if (x3) {
-    const size_t lds = (size_t)(3 * 64 * WX_ALD / 2 + 64 * w.WP) * sizeof(float);
-    hipLaunchKernelGGL(wgrad_x3_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
+    if constexpr (KG == 1) {
+      const size_t lds = (size_t)(3 * 64 * WX_ALD / 2 + 64 * w.WP) * sizeof(float);
+      hipLaunchKernelGGL(wgrad_x3_reg_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
+    } else {
+      const size_t lds = (size_t)(3 * 64 * WX_ALD / 2 + 3 * 64 * wx_xpw(w.W) / 2) * sizeof(float);
+      hipLaunchKernelGGL(wgrad_x3_kernel<KG>, dim3((unsigned)nblk), dim3(256), lds, st, w);
+    }
     return vrvq_launch_status();
   }
   const size_t lds = (size_t)(64 * ((1 << w.kt_sh) + 1) + 64 * w.WP) * sizeof(float);
