@@ -79,9 +79,9 @@ __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
 }
 
 // LDS bytes of one pipeline stage.
-template <int KS, int BM, int BN>
+template <int KS, int BM, bool PAIR>
 __host__ __device__ constexpr int x3_stage_w_bytes() {
-  return x3_pair<KS, BM, BN>() ? 2 * 3 * KS * BM * 16 : 3 * X3Cfg<KS>::NO2 * BM * 16;
+  return PAIR ? 2 * 3 * KS * BM * 16 : 3 * X3Cfg<KS>::NO2 * BM * 16;
 }
 __host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
 
@@ -90,9 +90,9 @@ __host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
 // Plain global loads (not LDS-DMA): the compiler then places the wait for them right before
 // the ds_write after the chunk's MFMAs; with LDS-DMA in inline asm it cannot see the loads and
 // its conservative waits at the next global load exposed their whole latency every chunk.
-template <int KS, int BM, int BN, int NT>
+template <int KS, int BM, bool PAIR, int NT>
 struct X3W {
-  static constexpr int TOTAL = x3_stage_w_bytes<KS, BM, BN>() / 16;  // uint4 per stage
+  static constexpr int TOTAL = x3_stage_w_bytes<KS, BM, PAIR>() / 16;  // uint4 per stage
   static constexpr int WQ = (TOTAL + NT - 1) / NT;                   // per thread
 };
 
@@ -101,20 +101,21 @@ struct X3W {
 // stride-1 windows only (a.ssh == 0), a.w3 = the pre-split weight.
 // PH: the phase-split view of a strided conv (ConvArgs::psh > 0; compile-time, so the stride-1
 // instantiations keep their plain window addressing).
-template <int BM, int BN, int WM, int NW, int KS, bool PH = false>
+template <int BM, int BN, int WM, int NW, int KS, bool PH = false,
+          bool PAIR = x3_pair<KS, BM, BN>()>
 __device__ __forceinline__ void conv_mainloop_x3(
     const ConvArgs& a, float* smem,
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
     int n0) {
   using TC = TileCfg<BM, BN, WM, NW>;
-  constexpr bool PAIR = x3_pair<KS, BM, BN>();
+  static_assert(!PAIR || (KS == 7 && !PH), "pair chunks: k7 stride-1 windows");
   using XC = X3Cfg<KS, PAIR>;
   constexpr int NO2P = X3Cfg<KS>::NO2;  // octet slots per packed (HBM) chunk
   constexpr int NT = TC::NT, RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
   constexpr int CK = XC::CK, NC8 = XC::NC8, NO = XC::NO, NO2 = XC::NO2, NSTEP = XC::NSTEP;
   constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
   constexpr int XI = (NC8 * XW_MAX + NT - 1) / NT;  // x items (octet, position) per thread
-  constexpr int WB = x3_stage_w_bytes<KS, BM, BN>();
+  constexpr int WB = x3_stage_w_bytes<KS, BM, PAIR>();
 
   const int XW = (BN - 1) + (KS - 1) * a.dil + 1;
   const int XWP = x3_xwp(XW);
@@ -134,7 +135,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
   char* sbase = reinterpret_cast<char*>(smem);
 
 
-  constexpr int WQ = X3W<KS, BM, BN, NT>::WQ, WTOT = X3W<KS, BM, BN, NT>::TOTAL;
+  constexpr int WQ = X3W<KS, BM, PAIR, NT>::WQ, WTOT = X3W<KS, BM, PAIR, NT>::TOTAL;
   u32x4 wr[WQ];
   auto load_w = [&](int chunk) {
 #pragma unroll
@@ -349,11 +350,11 @@ __device__ __forceinline__ void conv_mainloop_x3(
 }
 
 // LDS bytes the x3 mainloop needs for a window of XW positions.
-template <int KS, int BM, int BN>
+template <int KS, int BM, int BN, bool PAIR = x3_pair<KS, BM, BN>()>
 inline size_t x3_lds_bytes(int xw, int cin) {
-  const size_t xb = 3 * (size_t)X3Cfg<KS, x3_pair<KS, BM, BN>()>::NC8 * x3_xwp(xw) * 16;
-  const size_t snake = x3_pair<KS, BM, BN>() ? 2 * (size_t)cin * sizeof(float) : 0;
-  return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM, BN>() + xb) + snake;
+  const size_t xb = 3 * (size_t)X3Cfg<KS, PAIR>::NC8 * x3_xwp(xw) * 16;
+  const size_t snake = PAIR ? 2 * (size_t)cin * sizeof(float) : 0;
+  return x3_stages<BM, BN>() * ((size_t)x3_stage_w_bytes<KS, BM, PAIR>() + xb) + snake;
 }
 
 }  // namespace vrvq_conv
