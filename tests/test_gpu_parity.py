@@ -338,10 +338,14 @@ def test_conv1d_x3_vs_torch(case):
 
 @pytest.mark.parametrize("case", [(1, 256, 256, 4500, 7, 1, 3, 1, True, True, 0),
                                   (2, 384, 384, 4100, 7, 1, 27, 9, True, False, 0),
-                                  (1, 128, 320, 5000, 7, 1, 3, 1, False, True, 0)])
+                                  (1, 128, 320, 5000, 7, 1, 3, 1, False, True, 0),
+                                  (1, 384, 384, 4500, 1, 1, 0, 1, False, True, 0),
+                                  (2, 256, 512, 700, 1, 1, 0, 1, True, True, 0),
+                                  (2, 96, 128, 600, 1, 1, 0, 1, False, True, 0)])
 def test_conv1d_x3_long_rows_vs_torch(case):
-    """k7 x3 convs over rows of >= 4096 samples with >= 256 output channels: the shapes that take
-    the wide x3 tiles (VRVQ_CONV_X3_WIDE), ragged last tile and rows not a multiple of 64."""
+    """x3 convs on the pair-chunk tiles (conv_x3.h): k7 over rows of >= 640 samples with >= 128
+    output channels (VRVQ_CONV_X3_WIDE), the k1 + skip GEMMs (VRVQ_CONV_X3_K1PAIR), ragged last
+    tiles, and a Cin that is not a whole pair chunk (the fp32 loop on that tile)."""
     test_conv1d_x3_vs_torch(case)
 
 

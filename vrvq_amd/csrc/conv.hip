@@ -295,8 +295,10 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
     constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
     size_t lx = x3_lds_bytes<KS, BM, BN>(XW, a.cin);
     if (lx < epi) lx = epi;
+    // pair tiles (conv_x3.h) need whole K-chunks: other Cin take the fp32 loop on that tile
+    const bool pair_ok = !x3_pair<KS, BM, BN>() || a.cin % X3Cfg<KS, true>::CK == 0;
     if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
-        x3_tile_ok(BM, BN, KS, a)) {
+        x3_tile_ok(BM, BN, KS, a) && pair_ok) {
       if constexpr (KS == 2) {
         if (a.psh) {  // strided conv through the phase-split view
           if (lx > 64 * 1024) {

@@ -46,12 +46,15 @@ constexpr int x3_stages() { return BM * BN <= 128 * 128 ? 1 : 2; }
 // barriers instead of 96. The weight planes stay in the 8-channel packing (two packed chunks
 // per K-chunk, pad octets skipped while staging): 43 KB W + <= 30 KB x per stage, two
 // workgroups per CU.
+// A pair tile needs Cin to be a multiple of the K-chunk (launch_cfg falls back otherwise). The
+// k1 + skip GEMMs on the same construction (128 x 64 tiles, two 32-channel packed chunks per
+// K-chunk) measured slower: profiles/r03_x3_pair_ab.txt.
 template <int KS, int BM, int BN>
 constexpr bool x3_pair() { return KS == 7 && BM == 64 && BN == 256; }
 
 template <int KS, bool PAIR = false>
 struct X3Cfg {  // PAIR = false: also the HBM packing of the weight planes (vrvq_pack_x3_weight)
-  static constexpr int CK = PAIR ? 16 : KS == 1 ? 32 : KS <= 3 ? 16 : 8;  // channels per K-chunk
+  static constexpr int CK = (PAIR ? 2 : 1) * (KS == 1 ? 32 : KS <= 3 ? 16 : 8);  // channels per K-chunk
   static constexpr int NC8 = CK / 8;                        // channel octets per tap
   static constexpr int NO = KS * NC8;                       // octets per chunk
   static constexpr int NO2 = (NO + 1) & ~1;                 // padded to MFMA steps
@@ -81,7 +84,7 @@ __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
 // LDS bytes of one pipeline stage.
 template <int KS, int BM, bool PAIR>
 __host__ __device__ constexpr int x3_stage_w_bytes() {
-  return PAIR ? 2 * 3 * KS * BM * 16 : 3 * X3Cfg<KS>::NO2 * BM * 16;
+  return PAIR ? 2 * 3 * X3Cfg<KS>::NO * BM * 16 : 3 * X3Cfg<KS>::NO2 * BM * 16;
 }
 __host__ __device__ inline int x3_xwp(int xw) { return (xw + 3) & ~3; }
 
@@ -108,9 +111,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
     int n0) {
   using TC = TileCfg<BM, BN, WM, NW>;
-  static_assert(!PAIR || (KS == 7 && !PH), "pair chunks: k7 stride-1 windows");
+  static_assert(!PAIR || ((KS == 7 || KS == 1) && !PH), "pair chunks: k7 / k1 stride-1 windows");
   using XC = X3Cfg<KS, PAIR>;
   constexpr int NO2P = X3Cfg<KS>::NO2;  // octet slots per packed (HBM) chunk
+  constexpr int NOP = X3Cfg<KS>::NO;    // ... of them real (k7: 7 taps; k1: 4 channel octets)
+  constexpr int NC8P = X3Cfg<KS>::NC8;  // channel octets per packed chunk
+  static_assert(!PAIR || X3Cfg<KS, true>::NSTEP == NOP, "pair step q = packed octet q");
   constexpr int NT = TC::NT, RM = TC::RM, RN = TC::RN, TM = TC::TM, TN = TC::TN;
   constexpr int CK = XC::CK, NC8 = XC::NC8, NO = XC::NO, NO2 = XC::NO2, NSTEP = XC::NSTEP;
   constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
@@ -142,11 +148,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
     for (int r = 0; r < WQ; ++r) {
       const int u = min(tid + r * NT, WTOT - 1);  // clamped: no conditional load
       if constexpr (PAIR) {
-        // stage entry ((half * 3 + plane) * KS + tap) * BM + row <- packed chunk 2 chunk + half
-        const int hp = u / (KS * BM), r2 = u - hp * (KS * BM);
-        const int tap = r2 / BM, row = r2 - tap * BM;
+        // stage entry ((half * 3 + plane) * NOP + po) * BM + row <- octet po of packed chunk
+        // 2 chunk + half
+        const int hp = u / (NOP * BM), r2 = u - hp * (NOP * BM);
+        const int po = r2 / BM, row = r2 - po * BM;
         const int half = hp / 3, pl = hp - half * 3;
-        wr[r] = w3[(((size_t)(2 * chunk + half) * 3 + pl) * NO2P + tap) * a.m_pad + m0 + row];
+        wr[r] = w3[(((size_t)(2 * chunk + half) * 3 + pl) * NO2P + po) * a.m_pad + m0 + row];
       } else {
         const int po = u / BM, row = u - po * BM;
         wr[r] = w3[((size_t)chunk * 3 * NO2 + po) * a.m_pad + m0 + row];
@@ -254,16 +261,17 @@ __device__ __forceinline__ void conv_mainloop_x3(
   const int col = wn * TN + lr;
   auto rd_at = [&](const u32x4* ws, const u32x4* xs, int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
     // octet slot o = 2 q + lh: (tap, channel octet) in tap-major order; a pair chunk's slot
-    // (q, lh) is tap q of its packed chunk lh
+    // (q, lh) is octet q of its packed chunk lh: tap q / NC8P, channel octet
+    // lh * NC8P + q % NC8P of the staged window
     const int o = 2 * q + lh;
-    const int tap = PAIR ? q : o < NO ? o / NC8 : 0;  // padded octet: zero weights, any valid x
-    const int c8 = PAIR ? lh : o - (o / NC8) * NC8;
-    const int wo = PAIR ? lh * 3 * KS + q : o;  // + plane * (PAIR ? KS : NO2)
+    const int tap = PAIR ? q / NC8P : o < NO ? o / NC8 : 0;  // padded octet: zero weights, any valid x
+    const int c8 = PAIR ? lh * NC8P + q % NC8P : o - (o / NC8) * NC8;
+    const int wo = PAIR ? lh * 3 * NOP + q : o;  // + plane * (PAIR ? NOP : NO2)
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
       for (int i = 0; i < RM; ++i)
-        av[p][i] = ws[(p * (PAIR ? KS : NO2) + wo) * BM + wm * TM + i * 32 + lr];
+        av[p][i] = ws[(p * (PAIR ? NOP : NO2) + wo) * BM + wm * TM + i * 32 + lr];
     const int xo = c8 * XWP + col + tap * a.dil;
 #pragma unroll
     for (int p = 0; p < 3; ++p)
