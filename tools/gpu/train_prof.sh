@@ -1,0 +1,13 @@
+#!/bin/bash
+# Training step (configs[3] per GPU): bench --train and a rocprofv3 kernel trace of it.
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-trainprof}
+run() { local name=$1 to=$2; shift 2
+  echo "=== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/${T}_$name.log" 2>&1; local rc=$?
+  grep -v amdgpu.ids "gpurun_out/${T}_$name.log" | tail -${TAIL:-1} | cut -c1-300
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; return 0; }
+run bench 400 python bench.py --train --steps 3 --warmup 2
+run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py --train --steps 3 --warmup 2
+exit 0
