@@ -55,6 +55,13 @@ int vrvq_weight_norm(const float* g, const float* v, int rows, int cols, float* 
 /* inv[c] = 1 / (alpha[c] + 1e-9f). Snake's reciprocal, models/layers.py:30. */
 int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv, vrvq_stream_t stream);
 
+/* y[b,c,t] = snake_c(x[b,c,t]) = x + inv_alpha[c] * sin(alpha[c] * x)^2 (Snake1d forward,
+ * models/layers.py:26-32; the same per-element expression the conv kernels apply while
+ * staging). The training step's weight gradients take snake(x) from here once instead of
+ * re-evaluating it in every (row tile, chunk) that stages x. y may not alias x. */
+int vrvq_snake(const float* x, int batch, int channels, int frames, const float* alpha,
+               const float* inv_alpha, float* y, vrvq_stream_t stream);
+
 /* Codebook normalisation for VectorQuantize.decode_latents (models/quantize.py:92-99):
  * cbn[n,:] = cb[n,:] / max(||cb[n,:]||, 1e-12); c2[n] = sum_k cbn[n,k]^2.
  * cb is [rows][dim] (rows = nq * codebook_size for a stacked RVQ). */

@@ -21,6 +21,7 @@ _F = ctypes.c_float
 SIGNATURES = {
     "vrvq_weight_norm": [_P, _P, _I, _I, _P, _P],
     "vrvq_snake_inv_alpha": [_P, _I, _P, _P],
+    "vrvq_snake": [_P, _I, _I, _I, _P, _P, _P, _P],
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],

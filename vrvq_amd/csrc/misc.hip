@@ -264,6 +264,35 @@ extern "C" int vrvq_weight_norm(const float* g, const float* v, int rows, int co
   return vrvq_launch_status();
 }
 
+// Snake1d forward over [rows = batch * channels][frames]: one workgroup per (row, 1024-sample
+// segment), 4 samples per thread.
+__global__ __launch_bounds__(256) void snake_rows_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ alpha,
+                                                         const float* __restrict__ inv_alpha,
+                                                         int channels, int frames, int nseg,
+                                                         float* __restrict__ y) {
+  const int row = blockIdx.x / nseg, seg = blockIdx.x - row * nseg;
+  const int c = row % channels;
+  const float al = alpha[c], ia = inv_alpha[c];
+  const size_t base = (size_t)row * frames;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = seg * 1024 + u * 256 + (int)threadIdx.x;
+    if (t < frames) y[base + t] = snake_act(x[base + t], al, ia);
+  }
+}
+
+extern "C" int vrvq_snake(const float* x, int batch, int channels, int frames, const float* alpha,
+                          const float* inv_alpha, float* y, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && alpha && inv_alpha && y && x != y && batch > 0 && channels > 0 && frames > 0);
+  const int nseg = (frames + 1023) / 1024;
+  const long long nblk = (long long)batch * channels * nseg;
+  if (nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  hipLaunchKernelGGL(snake_rows_kernel, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), x,
+                     alpha, inv_alpha, channels, frames, nseg, y);
+  return vrvq_launch_status();
+}
+
 extern "C" int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv,
                                     vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(alpha && inv && channels > 0);

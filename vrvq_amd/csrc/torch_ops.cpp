@@ -621,15 +621,33 @@ Tensor conv1d_wgrad(const Tensor& a, const Tensor& x, int64_t k, int64_t stride,
   const int64_t B = a.size(0), M = a.size(1), TA = a.size(2), C = x.size(1), TX = x.size(2);
   if (alpha_a.has_value()) TORCH_CHECK(alpha_a->numel() == M, "conv1d_wgrad: alpha_a per row of a");
   if (alpha.has_value()) TORCH_CHECK(alpha->numel() == C, "conv1d_wgrad: alpha per channel of x");
+  // Snake of either operand once, up front (vrvq_snake: the staging expression, so the same
+  // values): the wgrad kernels would otherwise evaluate it in every row tile x chunk that
+  // stages the operand (M / 64 times over for x)
+  Tensor as_, xs_;
+  if (alpha_a.has_value()) {
+    as_ = at::empty_like(a);
+    check_rc(vrvq_snake(a.data_ptr<float>(), (int)B, (int)M, (int)TA, alpha_a->data_ptr<float>(),
+                        inv_alpha_a->data_ptr<float>(), as_.data_ptr<float>(), stream_of(a)),
+             "vrvq_snake");
+  }
+  if (alpha.has_value()) {
+    xs_ = at::empty_like(x);
+    check_rc(vrvq_snake(x.data_ptr<float>(), (int)B, (int)C, (int)TX, alpha->data_ptr<float>(),
+                        inv_alpha->data_ptr<float>(), xs_.data_ptr<float>(), stream_of(a)),
+             "vrvq_snake");
+  }
   int split = 0;
   long long bytes = 0;
   check_rc(vrvq_wgrad_plan((int)B, (int)M, (int)TA, (int)C, (int)k, &split, &bytes),
            "vrvq_wgrad_plan");
   Tensor ws = empty_f({(bytes + 3) / 4}, a);
   Tensor out = empty_f({M, C, k}, a);
-  check_rc(vrvq_conv1d_wgrad(a.data_ptr<float>(), (int)B, (int)M, (int)TA, fp(alpha_a),
-                             fp(inv_alpha_a), x.data_ptr<float>(), (int)C, (int)TX, fp(alpha),
-                             fp(inv_alpha), (int)k, (int)stride, (int)pad, (int)dil, split,
+  check_rc(vrvq_conv1d_wgrad(alpha_a.has_value() ? as_.data_ptr<float>() : a.data_ptr<float>(),
+                             (int)B, (int)M, (int)TA, nullptr, nullptr,
+                             alpha.has_value() ? xs_.data_ptr<float>() : x.data_ptr<float>(),
+                             (int)C, (int)TX, nullptr, nullptr, (int)k, (int)stride, (int)pad,
+                             (int)dil, split,
                              ws.data_ptr<float>(), (long long)ws.numel() * 4,
                              out.data_ptr<float>(), stream_of(a)),
            "vrvq_conv1d_wgrad");
