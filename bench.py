@@ -60,31 +60,31 @@ def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024)
     return B * T * per_frame + weights
 
 
-def newest(pattern: str):
-    """Newest (by round-tag name) configs[1] record; the configs[2]-shape records (*cfg3*) are
-    not this line's."""
+def newest(pattern: str, cfg3: bool = False):
+    """Newest (by round-tag name) record of the configs[1] shape, or with cfg3=True of the
+    configs[2] shape (B=64, 32 codebooks: the *cfg3* files)."""
     files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", pattern))
-                   if "cfg3" not in os.path.basename(f))
+                   if ("cfg3" in os.path.basename(f)) == cfg3)
     return files[-1] if files else None
 
 
-def rvq_pmc_traffic():
+def rvq_pmc_traffic(cfg3: bool = False):
     """HBM bytes per RVQ pass from the newest committed PMC measurement
     (profiles/*_rvq_pmc.json: rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the three
     kernels, separate passes, tools/gpu/pmc_rvq.sh at configs[1]). bench.py cannot collect PMC
     counters itself (they need their own rocprofv3 passes), so it reports that file."""
-    f = newest("*_rvq_pmc.json")
+    f = newest("*_rvq_pmc.json", cfg3)
     if f is None:
         return None, None
     d = json.load(open(f))
     return d.get("path_total_bytes"), os.path.relpath(f, REPO)
 
 
-def rvq_kernel_split():
+def rvq_kernel_split(cfg3: bool = False):
     """Per-kernel average duration (us) of the RVQ launches from the newest committed
     rocprofv3 kernel-stats summary (profiles/*_rvq_kernel_stats.csv)."""
     import csv
-    f = newest("*_rvq_kernel_stats.csv")
+    f = newest("*_rvq_kernel_stats.csv", cfg3)
     if f is None:
         return None, None
     out = {}
@@ -229,7 +229,7 @@ def train_main(args, world: int, rank: int, dev):
     import vrvq_amd
     from vrvq_amd.config import A2_KWARGS
     from vrvq_amd.recipe import load_recipe, synthetic_audio
-    from vrvq_amd.replicas import shard_seed, throughput, timed_steps
+    from vrvq_amd.replicas import shard_seed, sum_over_ranks, throughput, timed_steps
     from vrvq_amd.trainer import LAMBDAS_A2, build_state, train_step
     model = vrvq_amd.DAC_VRVQ(**A2_KWARGS)
     load_recipe(model, seed=0)
@@ -245,10 +245,12 @@ def train_main(args, world: int, rank: int, dev):
     ms = res_t.seconds / args.steps * 1e3
     value = throughput(args.batch * TRAIN_CLIP / SR, res_t)
     losses = {k: round(float(v), 5) for k, v in res_t.last.items()}
+    ranks_seen = int(sum_over_ranks([1.0], dev)[0])
     if rank == 0:
         print(json.dumps({
             "metric": "train audio-sec/s (vrvq_a2 generator+discriminator step, 0.38 s clips)",
             "value": round(value, 3), "unit": "audio-sec/s", "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic uniform audio [-0.5,0.5), recipe random-init weights",
@@ -344,7 +346,7 @@ def main(argv=None):
 
     import vrvq_amd
     from vrvq_amd.recipe import synthetic_audio
-    from vrvq_amd.replicas import job_rate, shard_seed, throughput, timed_steps
+    from vrvq_amd.replicas import job_rate, shard_seed, sum_over_ranks, throughput, timed_steps
 
     if args.train:
         train_main(args, world, rank, dev)
@@ -359,30 +361,30 @@ def main(argv=None):
     timer.install()
     nq = args.n_codebooks
     fps = math.floor(SR / model.hop_length)
-    lvl_ev = {lv: [] for lv in LEVELS}
+    lvl_ev = {"all": []}
 
     if args.sweep:
         # scripts/inference.py:88-112: encode once (level 1), then per level hard mask,
-        # masked sum of z_q_is, decode, bpf (device-side, no host sync inside the step)
+        # masked sum of z_q_is and bpf (device-side, no host sync inside the step); the four
+        # levels' z_q decoded as ONE batch of 4 x B clips (vrvq_amd.level_sweep)
         bits = torch.full((nq,), 10.0, device=dev)
+        from vrvq_amd.utils import sweep_latents
 
         def step():
             with torch.no_grad():
                 enc = model.encode(model.preprocess(audio, SR), None, 1.0)
-                out = []
-                for lv in LEVELS:
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    s = vrvq_amd.scale_importance(enc["imp_map"], lv * nq, 1.0)
-                    mask = vrvq_amd.generate_mask_hard(s, nq)
-                    y = model.decode(vrvq_amd.masked_sum(enc["z_q_is"], mask))
-                    bpf_t = vrvq_amd.ops.bpf(mask, bits)
-                    e1.record()
-                    if timer.enabled:
-                        lvl_ev[lv].append((e0, e1))
-                    out.append((lv, mask, bpf_t, y))
-                return out
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                masks, z_all = sweep_latents(enc["imp_map"], enc["z_q_is"], LEVELS, nq)
+                y = model.decode(z_all)
+                bpfs = [vrvq_amd.ops.bpf(m, bits) for m in masks]
+                e1.record()
+                if timer.enabled:
+                    lvl_ev["all"].append((e0, e1))
+                B = args.batch
+                return [(lv, masks[i], bpfs[i], y[i * B:(i + 1) * B])
+                        for i, lv in enumerate(LEVELS)]
     else:
         def step():
             with torch.no_grad():
@@ -407,20 +409,21 @@ def main(argv=None):
     levels_rep = None
     if args.sweep:
         levels_rep = []
+        ms = float(np.mean([a.elapsed_time(b) for a, b in lvl_ev["all"]]))
         for lv, mask, bpf_t, _y in res_t.last:
             rep = job_rate(args.batch * CLIP_SAMPLES / SR, float((mask.double() * 10.0).sum()),
                            mask.shape[0] * mask.shape[2], fps, device=dev)
-            ms = float(np.mean([a.elapsed_time(b) for a, b in lvl_ev[lv]]))
             levels_rep.append({"level": lv, "bpf": round(rep.bpf, 6), "kbps": round(rep.kbps, 4),
                                "bpf_rank0_kernel": round(float(bpf_t), 6),
-                               "decode_ms_rank0": round(ms, 3),
-                               "decode_audio_sec_per_s": round(rep.audio_seconds /
-                                                               (ms * 1e-3), 2)})
+                               "decode_ms_all_levels_rank0": round(ms, 3),
+                               "decode_audio_sec_per_s_all_levels": round(
+                                   len(LEVELS) * rep.audio_seconds / (ms * 1e-3), 2)})
     conv_ms = ms_per_step - rvq_ms
     conv_tflops = flops / (conv_ms * 1e-3) / 1e12
-    cfg2 = (args.batch, nq) == (32, 8) and not args.sweep
-    traffic, traffic_src = rvq_pmc_traffic() if cfg2 else (None, None)
-    split, split_src = rvq_kernel_split() if cfg2 else (None, None)
+    shape = {(32, 8): False, (64, 32): True}.get((args.batch, nq)) if not args.sweep else None
+    traffic, traffic_src = rvq_pmc_traffic(shape) if shape is not None else (None, None)
+    split, split_src = rvq_kernel_split(shape) if shape is not None else (None, None)
+    ranks_seen = int(sum_over_ranks([1.0], dev)[0])
     if rank == 0:
         workload = ("DAC_VRVQ conf/base.yml VBR, level sweep {0.25,0.5,1,2}: encode once + per "
                     "level mask/masked-sum/decode/bpf (scripts/inference.py:88-112)"
@@ -432,6 +435,7 @@ def main(argv=None):
             "value": round(value, 3),
             "unit": "audio-sec/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),

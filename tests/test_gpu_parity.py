@@ -343,9 +343,10 @@ def test_conv1d_x3_vs_torch(case):
                                   (2, 256, 512, 700, 1, 1, 0, 1, True, True, 0),
                                   (2, 96, 128, 600, 1, 1, 0, 1, False, True, 0)])
 def test_conv1d_x3_long_rows_vs_torch(case):
-    """x3 convs on the pair-chunk tiles (conv_x3.h): k7 over rows of >= 640 samples with >= 128
-    output channels (VRVQ_CONV_X3_WIDE), the k1 + skip GEMMs (VRVQ_CONV_X3_K1PAIR), ragged last
-    tiles, and a Cin that is not a whole pair chunk (the fp32 loop on that tile)."""
+    """x3 convs over long rows: k7 over rows of >= 640 samples with >= 128 output channels and
+    Cin % 16 == 0 (the pair-chunk 64 x 256 tiles of conv_x3.h; dispatch_tiles takes them only
+    for such Cin, so launch_cfg's pair_ok guard is defensive), the k1 + skip GEMMs on their
+    8-channel chunks, and ragged last tiles."""
     test_conv1d_x3_vs_torch(case)
 
 

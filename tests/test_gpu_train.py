@@ -145,6 +145,39 @@ def test_wgrad_deterministic():
     assert l2rel(r1.cpu().numpy(), ref.numpy()) < TOL
 
 
+@pytest.mark.parametrize("m,c,k,stride,pad,dil,T", [
+    (96, 64, 7, 1, 9, 3, 300),     # wgrad_x3_kernel (stride-1 taps)
+    (64, 96, 1, 1, 0, 1, 257),     # wgrad_x3_reg_kernel (k = 1)
+    (128, 64, 4, 2, 1, 1, 128),    # wgrad_kernel (strided, fp32-input MFMA)
+])
+def test_wgrad_c_abi_in_kernel_snake(m, c, k, stride, pad, dil, T):
+    """vrvq_conv1d_wgrad with alpha / alpha_a set (the Snake applied by the kernels while they
+    stage the operands) returns the same bits as the torch op's path (Snake precomputed by
+    vrvq_snake, nullptr alphas): the public C entry point the op no longer takes, per kernel."""
+    from vrvq_amd import _lib
+    import ctypes
+    g0 = torch.Generator().manual_seed(m + c + k)
+    B = 2
+    ta = (T + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    a = torch.randn(B, m, ta, generator=g0).to(DEV)
+    x = torch.randn(B, c, T, generator=g0).to(DEV)
+    al_a = (torch.rand(m, generator=g0) + 0.5).to(DEV)
+    al_x = (torch.rand(c, generator=g0) + 0.5).to(DEV)
+    inv_a, inv_x = ops.snake_inv_alpha(al_a), ops.snake_inv_alpha(al_x)
+    want = ops.conv1d_wgrad(a, x, k, stride, pad, dil, snake_a=(al_a, inv_a),
+                            snake_x=(al_x, inv_x))
+    split, ws_bytes = ctypes.c_int(0), ctypes.c_longlong(0)
+    _lib.call("vrvq_wgrad_plan", B, m, ta, c, k, ctypes.byref(split), ctypes.byref(ws_bytes))
+    ws = torch.empty((ws_bytes.value + 3) // 4, device=DEV)
+    out = torch.empty(m, c, k, device=DEV)
+    P = lambda v: ctypes.c_void_p(v.data_ptr())  # noqa: E731
+    _lib.call("vrvq_conv1d_wgrad", P(a), B, m, ta, P(al_a), P(inv_a), P(x), c, T, P(al_x),
+              P(inv_x), k, stride, pad, dil, split.value, P(ws), ws.numel() * 4, P(out),
+              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
+
+
 # ------------------------------------------------------------------ mask STE
 def logcosh64(alpha, pmk):  # models/utils.py:11-32 restated
     EPS = 1e-10

@@ -136,9 +136,12 @@ def test_a2_kwargs_match_reference_config(manifest):
 
 def test_unknown_lambda_key_raises():
     """scripts/train.py:319 sums every lambda key: a misspelt key is a KeyError, raised before
-    any work; the VBR rate keys are accepted (a CBR model contributes no rate term)."""
+    any work; the VBR rate keys only where the generator has an importance subnet (a CBR model
+    has no rate term: a KeyError in the reference too)."""
     from vrvq_amd.trainer import LAMBDAS_A2, check_lambdas
     check_lambdas(LAMBDAS_A2)
     check_lambdas({"mel/loss": 15.0, "vq/rate_loss": 2.0})
+    with pytest.raises(KeyError, match="rate_loss"):
+        check_lambdas({"mel/loss": 15.0, "vq/rate_loss": 2.0}, has_rate=False)
     with pytest.raises(KeyError, match="mel/los"):
         check_lambdas({**LAMBDAS_A2, "mel/los": 1.0})

@@ -173,7 +173,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
   // W DMA issued before it: the whole memory latency exposed once per chunk.)
   // pair tiles: every input channel's Snake parameters in LDS behind the stage (their 16 per
   // chunk do not fit the scalar registers)
-  float* snl = reinterpret_cast<float*>(sbase + STG);
+  float* snl = reinterpret_cast<float*>(sbase + X3_STAGES * STG);  // after every stage
   auto load_x = [&](int ci0) {
 #pragma unroll
     for (int it = 0; it < XI; ++it) {

@@ -45,6 +45,10 @@ constexpr int CH_NQMAX = 32;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr int CPOL_SC1 = 16;    // buffer load / store aux: sc1 (L1 bypass, write-through)
+constexpr int RSRC_FLAGS = 0x00020000;  // raw buffer descriptor word 3 (gfx950)
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
@@ -237,13 +241,29 @@ constexpr int PJ2_LD = 112;                     // z_s row stride (112 = 48 mod 
                                                 // of the B reads land on disjoint bank ranges)
 constexpr int PJ2_ZQ = PJ_KC * PJ2_TC / PJ2_NT; // z loads per thread per K chunk (6)
 
-__global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __restrict__ z, int T,
-                                                              int nq, int n_tc,
-                                                              const float* __restrict__ w_in_t,
-                                                              float* __restrict__ part, int NF) {
-  __shared__ __attribute__((aligned(16))) float z_s[PJ_CPS * PJ2_LD];
-  const int tc = blockIdx.x % n_tc, b = blockIdx.x / n_tc;
-  const int s = blockIdx.y;
+// Where the partials go: plain stores (the three-launch path: the chain reads them after a
+// kernel boundary) or write-through sc1 16-B stores (the fused launch: read by other workgroups
+// of the same launch with sc1 loads, MI355X_MICROARCH.md visibility table, first row).
+struct PartSink {
+  float* part;
+  __amdgpu_buffer_rsrc_t rsrc;
+  bool sc1;
+  __device__ __forceinline__ void put(size_t off, float4 v) const {
+    if (sc1) {
+      u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                 __float_as_uint(v.w)};
+      __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, (int)(off * 4), 0, CPOL_SC1);
+    } else {
+      *reinterpret_cast<float4*>(part + off) = v;
+    }
+  }
+};
+
+// One (clip b, frame tile tc, channel split s) projection unit; z_s = PJ_CPS * PJ2_LD floats
+// of LDS.
+__device__ __forceinline__ void project2_body(const float* __restrict__ z, int T, int nq, int tc,
+                                              int b, int s, const float* __restrict__ w_in_t,
+                                              const PartSink& out, int NF, float* z_s) {
   const int R = nq * RCD;
   const int t0 = tc * PJ2_TC;
   const int ntl = min(PJ2_TC, T - t0);
@@ -313,8 +333,8 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __res
         const int t = ch * 48 + q * 16 + lr;
         if (t < ntl) {
           const size_t n = (size_t)b * T + t0 + t;
-          *reinterpret_cast<float4*>(part + ((size_t)s * NF + n) * R + rr) =
-              make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+          out.put(((size_t)s * NF + n) * R + rr,
+                  make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]));
         }
       }
     }
@@ -323,6 +343,15 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __res
       for (int j = 0; j < PJ_CPS / 4; ++j) av[j] = an[j];
     }
   }
+}
+
+__global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __restrict__ z, int T,
+                                                              int nq, int n_tc,
+                                                              const float* __restrict__ w_in_t,
+                                                              float* __restrict__ part, int NF) {
+  __shared__ __attribute__((aligned(16))) float z_s[PJ_CPS * PJ2_LD];
+  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), false};
+  project2_body(z, T, nq, blockIdx.x % n_tc, blockIdx.x / n_tc, blockIdx.y, w_in_t, out, NF, z_s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -400,12 +429,60 @@ struct ChainLds {
   }
 };
 
-template <int NM>
-__global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
+// ------------------------------------------------------------------------------------------
+// In-launch hand-offs of the fused path (rvq_fused_kernel). Every shared word is a global
+// agent-scope access; payloads are stored write-through (sc1) by the producing wave, which drains
+// them (s_waitcnt vmcnt(0)) before ONE lane stores the flag; consumers poll the flag with sc1
+// loads from one wave and read the payload with sc1 loads after a workgroup barrier
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the valid-forms table). Flags
+// are monotonic per call: projection unit done = epoch, chain part published k stages =
+// 64 epoch + k (epochs grow per call on a stream: stale words of older calls are smaller).
+constexpr unsigned SPIN_MAX = 1u << 19;  // bounded spins (~0.5 s); on the bound: *err = code
+
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
+  __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: lanes < n poll flags[lane] until every one is >= target. Returns the smallest word
+// seen (>= target), or 0 after SPIN_MAX polls (then *err = code).
+__device__ __forceinline__ unsigned wave_wait_ge(const unsigned* flags, int n, unsigned target,
+                                                 unsigned* err, unsigned code) {
+  const int lane = threadIdx.x & 63;
+  const unsigned* p = flags + (lane < n ? lane : 0);
+  for (unsigned it = 0; it < SPIN_MAX; ++it) {
+    const unsigned v = ld_flag(p);
+    if (__builtin_amdgcn_ballot_w64(lane < n && v < target) == 0) {
+      unsigned mn = 0xffffffffu;
+      for (int l = 0; l < n; ++l) mn = min(mn, (unsigned)__builtin_amdgcn_readlane((int)v, l));
+      return mn;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (lane == 0) st_flag(err, code);
+  return 0;
+}
+
+struct ChainHandoff {              // fused launch only
+  const unsigned* flagp;           // the clip's projection-unit words (PJ_SPLIT)
+  unsigned* flagc;                 // this chain part's publish word
+  unsigned* err;
+  unsigned epoch;
+  __amdgpu_buffer_rsrc_t part;     // the partials, read with sc1 loads
+  __amdgpu_buffer_rsrc_t zsh;      // the stage hand-off rows, stored sc1
+  int zsh0;                        // float offset of (clip, stage 0, this part)
+  int zsh_stage;                   // floats per stage
+};
+
+template <int NM, bool FUSED>
+__device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0, int nf,
+                                           const ChainHandoff& hx) {
   constexpr int N = 256 * NM;
   constexpr int NPW = N / CH_NW;   // codes per wave
   constexpr int NT = NPW / 16;     // 16-code MFMA tiles per wave
-  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int nq = a.nq, F = a.F;
   const ChainLds L(nq, F, N);
   float* e_s = sm + L.e;
@@ -421,8 +498,6 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
   float* c2_s = sm + L.c2;      // [2][N]
   float* m_s = sm + L.m;        // [3][nq][8][8]: M_{.,j} for j = i-1, i, i+1 (mod 3)
 
-  const int n0 = blockIdx.x * F;
-  const int nf = min(F, a.NF - n0);
   const int R = nq * RCD;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -433,6 +508,27 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
   CSTAMP(nq, 0);
 
   // ---- prologue: pu = (P + b_in) - Qb (partials summed in split order); stage 0 operands.
+  if constexpr (FUSED) {
+    // wait for the clip's PJ_SPLIT projection units, then read the partials write-through
+    // (sc1) as float4: nf * R / 4 per split (R = 8 nq, the frames' rows are contiguous)
+    if (wave == 0) wave_wait_ge(hx.flagp, PJ_SPLIT, hx.epoch, hx.err, 1u);
+    __syncthreads();
+    for (int e4 = tid; e4 < nf * R / 4; e4 += CH_NT) {
+      u32x4 v[PJ_SPLIT];
+#pragma unroll
+      for (int sp = 0; sp < PJ_SPLIT; ++sp)
+        v[sp] = __builtin_amdgcn_raw_buffer_load_b128(
+            hx.part, (int)((((size_t)sp * a.NF + n0) * R + 4 * e4) * 4), 0, CPOL_SC1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pv = __uint_as_float(v[0][j]);
+#pragma unroll
+        for (int sp = 1; sp < PJ_SPLIT; ++sp) pv = pv + __uint_as_float(v[sp][j]);
+        const int e = 4 * e4 + j, r = e % R;
+        pu_s[e] = (pv + a.b_in[r]) - a.qb[r];
+      }
+    }
+  } else
   // Two (frame, row) items per thread per pass with all 16 partial loads in flight.
   for (int e0 = tid; e0 < nf * R; e0 += 2 * CH_NT) {
     float v[2][PJ_SPLIT];
@@ -608,6 +704,15 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
     CSTAMP(i, 3);
     __syncthreads();  // ------------------------------- candidates, stage i+1's c2 / M ready
     CSTAMP(i, 4);
+    if constexpr (FUSED) {
+      // the S2 waves publish stage i-1: its zst rows were stored write-through in S2 of stage
+      // i-1 (a stage ago, so this drain waits for nothing but this stage's prefetch, which the
+      // end of S2 needs anyway); each wave signals for its own stores
+      if (wave < 2 && i > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_flag(hx.flagc + wave, hx.epoch * 64u + (unsigned)i);
+      }
+    }
     // ---- S2 (role lanes) ----
     int bi = 0;
     float zq = 0.0f;
@@ -631,6 +736,13 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
       zq = cr_s[(rf * CH_NW + bw) * RCD + rk];  // raw codebook row of the winner
     }
     const float zsv = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
+    if constexpr (FUSED) {
+      // waves 0-1 = frames 0..15 x k: the part's 16-frame row block of this stage, two whole
+      // 256-B runs (frames >= nf store 0), one sc1 store per wave
+      if (wave < 2)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsv), hx.zsh,
+                                              (hx.zsh0 + i * hx.zsh_stage + tid) * 4, 0, CPOL_SC1);
+    }
     const float diff = ze - zq;
     const float l2 = vrvq::sum8(diff * diff, lane);
     if (role) {
@@ -664,6 +776,12 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
     CSTAMP(i, 7);
   }
   CSTAMP(nq, 2);
+  if constexpr (FUSED) {  // publish the last stage
+    if (wave < 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) st_flag(hx.flagc + wave, hx.epoch * 64u + (unsigned)nq);
+    }
+  }
 
   // ---- epilogue: outputs of every stage (LDS -> HBM)
   for (int e = tid; e < nf * nq * RCD; e += CH_NT) {
@@ -671,7 +789,7 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
     const int k = e & 7, fi = e >> 3;
     const int i = fi / nf, f = fi - i * nf;
     const int n = n0 + f, b = n / a.T, t = n - b * a.T;
-    a.zst[(((size_t)b * nq + i) * a.T + t) * RCD + k] = zs_s[(f * nq + i) * RCD + k];
+    if (a.zst) a.zst[(((size_t)b * nq + i) * a.T + t) * RCD + k] = zs_s[(f * nq + i) * RCD + k];
     a.latents[(((size_t)b * nq + i) * RCD + k) * a.T + t] = lat_s[(f * nq + i) * RCD + k];
   }
   for (int e = tid; e < nf * nq; e += CH_NT) {
@@ -686,6 +804,13 @@ __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
     }
   }
   CSTAMP(nq, 3);
+}
+
+template <int NM>
+__global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n0 = blockIdx.x * a.F;
+  chain_body<NM, false>(a, sm, n0, min(a.F, a.NF - n0), ChainHandoff{});
 }
 
 // ------------------------------------------------------------------------------------------

@@ -315,8 +315,10 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
         else:
             mode = "CBR"
             if int(n_quantizers) < nq:
-                # The reference stacks n_quantizers z_q_i against an (B, Nq, T) mask of ones and
-                # fails with a shape mismatch at models/quantize.py:421.
+                # The reference stacks n_quantizers z_q_i against an (B, Nq, T) mask of ones at
+                # models/quantize.py:421: 2 <= n < Nq is a shape mismatch there,
+                # n = 0 fails at torch.stack, and n = 1 broadcasts to z_q = (sum of the Nq mask
+                # rows) * z_q_0. All three raise here (n = 1 is a known difference).
                 raise RuntimeError(
                     f"VBRResidualVectorQuantize in CBR mode needs n_quantizers >= n_codebooks "
                     f"({n_quantizers} < {nq}), as in the reference")

@@ -312,8 +312,10 @@ def vbr_cbr_forward(q, z, n_quantizers: int):
     """VBRResidualVectorQuantize.forward in training mode with n_quantizers given (CBR mode,
     models/quantize.py:346-414): every stage runs, the importance rows of the mask are ones
     (no level draw, no importance map), then the dropout and full-codebook rows. The only draw
-    is the dropout randint (:406). n_quantizers < Nq fails in the reference (shape mismatch
-    at :421) and raises here."""
+    is the dropout randint (:406). n_quantizers < Nq raises here. In the reference 2 <= n < Nq
+    is a shape mismatch at :421 and n = 0 fails at torch.stack, but n = 1 broadcasts the one
+    stage against the (B, Nq, T) mask (z_q = sum of the mask rows * z_q_0): that value is a
+    known difference."""
     B, D, T = z.shape
     nq = q.n_codebooks
     if int(n_quantizers) < nq:

@@ -75,11 +75,11 @@ LOSS_KEYS = ("adv/disc_loss", "stft/loss", "mel/loss", "waveform/loss", "adv/gen
 RATE_KEYS = ("vq/rate_loss", "vq/rate_loss_scaled")
 
 
-def check_lambdas(lambdas: Dict[str, float]) -> None:
+def check_lambdas(lambdas: Dict[str, float], has_rate: bool = True) -> None:
     """scripts/train.py:319 sums `v * output[k]` over every lambda key, so a key with no loss
-    term is a KeyError there; raised here before any work. The one allowance: the rate terms of
-    a VBR lambda set on a CBR model (no importance map), which contribute nothing."""
-    known = set(LOSS_KEYS) | set(RATE_KEYS)
+    term is a KeyError there; raised here before any work. The rate terms exist only for a
+    generator with an importance subnet (has_rate): on a CBR model they are KeyErrors too."""
+    known = set(LOSS_KEYS) | (set(RATE_KEYS) if has_rate else set())
     missing = [k for k in lambdas if k not in known]
     if missing:
         raise KeyError(f"train_step: lambda keys with no loss term: {missing}")
@@ -91,7 +91,7 @@ def train_step(state: State, audio: torch.Tensor, lambdas: Dict[str, float] = LA
     generator forward (train mode), discriminator update, generator losses + update. Returns the
     loss / norm tensors (device tensors: no host sync here)."""
     gen, disc = state.generator, state.discriminator
-    check_lambdas(lambdas)
+    check_lambdas(lambdas, hasattr(unwrap(gen).quantizer, "imp_subnet"))
     gen.train()
     disc.train()
     n_codebooks = unwrap(gen).n_codebooks
@@ -116,7 +116,7 @@ def train_step(state: State, audio: torch.Tensor, lambdas: Dict[str, float] = LA
     if imp_map is not None:
         out["vq/rate_loss"] = imp_map.mean()
         out["vq/rate_loss_scaled"] = out["vq/rate_loss"] * n_codebooks
-    out["loss"] = sum(v * out[k] for k, v in lambdas.items() if k in out)
+    out["loss"] = sum(v * out[k] for k, v in lambdas.items())
 
     state.optimizer_g.zero_grad(set_to_none=True)
     out["loss"].backward()

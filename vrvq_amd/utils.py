@@ -58,26 +58,37 @@ def masked_sum(z_q_is: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return ops.masked_sum(z_q_is.contiguous(), mask.contiguous())
 
 
+def sweep_latents(imp_map: torch.Tensor, z_q_is: torch.Tensor, levels: Sequence[float],
+                  n_q: int):
+    """Per level: hard mask of imp_map * (level * Nq) and the masked sum of z_q_is
+    (scripts/inference.py:95-100). Returns (masks, z_q stacked level-major as (L*B, D, T))."""
+    masks = [generate_mask_hard(scale_importance(imp_map, level * n_q, 1.0), n_q)
+             for level in levels]
+    return masks, torch.cat([masked_sum(z_q_is, m) for m in masks])
+
+
 def level_sweep(model, audio: torch.Tensor, levels: Sequence[float], bits_per_codebook: int = 10,
                 decode: bool = True):
     """The reference's VBR level sweep (scripts/inference.py:88-112) without file I/O.
 
     Encodes once (level 1), then for each level: hard mask of imp_map * (level * Nq),
-    masked sum of z_q_is, decode, bpf and kbps. Returns a list of dicts."""
+    masked sum of z_q_is, bpf and kbps. The levels' z_q go through ONE decode of L*B clips
+    (the reference decodes level by level; clips are independent and the decoder is batch
+    invariant, so the per-level outputs are the same — tests/test_gpu_parity.py checks the
+    batched recon against the reference's per-level fixtures). Returns a list of dicts."""
     n_q = model.n_codebooks
     with torch.no_grad():
         x = model.preprocess(audio, model.sample_rate)
         enc = model.encode(x, n_quantizers=None, level=1)
-    imp_map = enc["imp_map"]
+        masks, z_all = sweep_latents(enc["imp_map"], enc["z_q_is"], levels, n_q)
+        recon_all = model.decode(z_all) if decode else None
+    B = audio.shape[0]
     out = []
-    for level in levels:
-        level_scaled = level * n_q
-        s = scale_importance(imp_map, level_scaled, 1.0)
-        mask = generate_mask_hard(s, n_q)
-        z_q = masked_sum(enc["z_q_is"], mask)
-        recon = model.decode(z_q) if decode else None
+    for li, level in enumerate(levels):
+        mask = masks[li]
         bpf = cal_bpf_from_mask(mask, [bits_per_codebook] * n_q)
         kbps = bpf * math.floor(model.sample_rate / model.hop_length) / 1000
-        out.append({"level": level, "level_scaled": level_scaled, "mask": mask, "z_q": z_q,
-                    "recon": recon, "bpf": bpf, "kbps": kbps})
+        recon = recon_all[li * B:(li + 1) * B] if decode else None
+        out.append({"level": level, "level_scaled": level * n_q, "mask": mask,
+                    "z_q": z_all[li * B:(li + 1) * B], "recon": recon, "bpf": bpf, "kbps": kbps})
     return out
