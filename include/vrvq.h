@@ -217,14 +217,32 @@ int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
  * 2), or VRVQ_ERR_ARG. */
 int vrvq_rvq_project_variant(int variant);
 
-/* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows). */
+/* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows /
+ * the fused launch's stage hand-off rows, whichever is larger). */
 int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
 
-/* The whole quantizer in three stream-ordered launches (project -> chain -> expand), the
- * replacement of VBRResidualVectorQuantize.forward's quantizer loop, importance mask and masked
- * sum (models/quantize.py:353-365, 389-421) and of ResidualVectorQuantize.forward in eval
- * (:136-214). workspace: >= vrvq_rvq_workspace() bytes, 16-byte aligned, caller-owned, no
- * initialisation needed. */
+/* RVQ launch structure of vrvq_rvq_encode (process-wide): 2 = ONE fused launch where the shape
+ * allows it (frames <= 96; up to 32 clips per launch, more clips run as consecutive launches),
+ * else three launches (default); 1 = always the three launches (also VRVQ_RVQ_FUSED=0 in the
+ * environment). Both give the same outputs bit for bit. path 0 queries. Returns the previous
+ * path (1 or 2), or VRVQ_ERR_ARG. */
+int vrvq_rvq_path(int path);
+
+/* The fused launch's in-kernel waits are bounded: a wait that runs out (a hang averted: it
+ * cannot happen with the whole grid resident) records a code in the stream's flag block and the
+ * launch runs on with garbage. *code = that code (1 projection wait, 2 stage wait) or 0, and it
+ * is cleared. Synchronises the stream. */
+int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code);
+
+/* The whole quantizer, the replacement of VBRResidualVectorQuantize.forward's quantizer loop,
+ * importance mask and masked sum (models/quantize.py:353-365, 389-421) and of
+ * ResidualVectorQuantize.forward in eval (:136-214): one fused launch (projection units, chain
+ * parts that publish every stage's zst rows, expansion workgroups that write z_q_is / z_q
+ * under the chain; see vrvq_rvq_path) or three stream-ordered launches (project -> chain ->
+ * expand, the steps below). The fused launches of a stream share a small flag block the library
+ * allocates on first use (hipMalloc, outside any stream capture); under stream capture a memset
+ * of it is captured in front of each launch. workspace: >= vrvq_rvq_workspace() bytes, 16-byte
+ * aligned, caller-owned, no initialisation needed. */
 int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
                     const float* w_in_t, const float* b_in, const float* cb, const float* cbf,
                     const float* c2, const float* w_out, const float* b_out, const float* mcol,

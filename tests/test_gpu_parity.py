@@ -476,12 +476,12 @@ def _check_clips(out, enc, ref, sel):
     assert torch.equal(vrvq_amd.masked_sum(enc["z_q_is"], enc["mask_imp"]), enc["z_q"])
 
 
-CFG2_CLIPS = (0, 5, 9, 14, 18, 23, 27, 31)
+CFG2_CLIPS = tuple(range(32))
 
 
 def test_config2_full_batch_vs_oracle(manifest):
-    """BASELINE config 2: conf/base.yml (8 cb VBR), B = 32 x 1 s, level 1: 8 clips spread over
-    the batch vs the oracle (models/dac_vrvq.py:222-252)."""
+    """BASELINE config 2: conf/base.yml (8 cb VBR), B = 32 x 1 s, level 1: every clip of the
+    batch vs the oracle (models/dac_vrvq.py:222-252)."""
     _model, _a, out, enc, _o, ref = _full_run(manifest, "golden_nq8", 32, sel=CFG2_CLIPS)
     assert out["codes"].shape == (32, 8, 87) and out["audio"].shape == (32, 1, 44100)
     _check_clips(out, enc, ref, CFG2_CLIPS)
@@ -490,8 +490,8 @@ def test_config2_full_batch_vs_oracle(manifest):
 @pytest.mark.parametrize("nq", [28, 32])
 def test_config3_full_batch_vs_oracle(manifest, nq):
     """BASELINE config 3: conf/base_24kbps.yml (n_codebooks 28 as in the file, and the 32
-    override), B = 64, whole model: 4 clips spread over the batch vs the oracle."""
-    sel = (0, 21, 42, 63)
+    override), B = 64, whole model: 16 clips spread over the batch vs the oracle."""
+    sel = tuple(range(0, 64, 4)) + (63,)
     _model, _a, out, enc, _o, ref = _full_run(manifest, "golden_nq28", 64, nq=nq, sel=sel, seed=77)
     assert out["codes"].shape == (64, nq, 87)
     _check_clips(out, enc, ref, sel)
@@ -499,7 +499,7 @@ def test_config3_full_batch_vs_oracle(manifest, nq):
 
 def test_level_sweep_full_batch_vs_oracle(manifest):
     """scripts/inference.py:88-112 at B = 32 (BASELINE config 5's per-GPU shape x2): for every
-    level, masks bit-exact and z_q within 1e-4 on the 8 oracle clips, recon of 2 clips vs the
+    level, masks bit-exact and z_q within 1e-4 on every clip, recon of 8 clips vs the
     oracle decoder, bpf / kbps over the whole batch equal to the reference formula on the
     masks (models/utils.py:64-73) and, over the oracle clips, to the oracle's own bpf."""
     from oracle.vrvq_oracle import cal_bpf_from_mask as bpf_np, generate_mask_hard as mask_np
@@ -515,8 +515,9 @@ def test_level_sweep_full_batch_vs_oracle(manifest):
         mask = r["mask"].cpu().numpy()
         np.testing.assert_array_equal(mask[sel], m_ref)
         assert rel_err(r["z_q"][sel].cpu().numpy(), msum_np(ref["z_q_is"], m_ref)) < TOL
-        y = o.decoder(msum_np(ref["z_q_is"][:2], m_ref[:2]))
-        assert rel_err(r["recon"][sel[:2]].cpu().numpy(), y) < TOL
+        pick = sel[::4]  # 8 clips spread over the batch
+        y = o.decoder(msum_np(ref["z_q_is"][pick], m_ref[pick]))
+        assert rel_err(r["recon"][pick].cpu().numpy(), y) < TOL
         assert r["bpf"] == pytest.approx(bpf_np(mask, [10] * nq), rel=1e-6)
         assert r["kbps"] == pytest.approx(r["bpf"] * 86 / 1000, rel=1e-12)
         sub = vrvq_amd.cal_bpf_from_mask(r["mask"][sel].contiguous(), [10] * nq)
@@ -664,6 +665,7 @@ def test_rvq_projection_variants_bit_identical(nq, B, T):
     imp = torch.rand(B, T, generator=gen).to(DEV)
     outs = {}
     prev = _lib.rvq_project_variant(0)
+    prev_path = _lib.rvq_path(1)  # the three launches: the variants are their first kernel
     try:
         for v in (1, 2):
             _lib.rvq_project_variant(v)
@@ -671,8 +673,97 @@ def test_rvq_projection_variants_bit_identical(nq, B, T):
             torch.cuda.synchronize()
     finally:
         _lib.rvq_project_variant(prev)
+        _lib.rvq_path(prev_path)
     for a, b in zip(outs[1], outs[2]):
         assert (a is None and b is None) or torch.equal(a, b)
+
+
+def _rvq_both_paths(nq, ncode, B, T, imp_on, zqis, seed, repeats=3, side_load=False):
+    from vrvq_amd import _lib
+    q, gen = _random_rvq(nq, ncode, seed)
+    st = q.stacked()
+    z = (torch.randn(B, 1024, T, generator=gen) * 0.3).to(DEV)
+    imp = torch.rand(B, T, generator=gen).to(DEV) if imp_on else None
+    run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=0.8,  # noqa: E731
+                                 want_z_q_is=zqis)
+    prev = _lib.rvq_path(1)
+    try:
+        want = run()
+        torch.cuda.synchronize()
+        _lib.rvq_path(2)
+        got = []
+        side = torch.cuda.Stream() if side_load else None
+        a = torch.randn(2048, 2048, device=DEV) if side_load else None
+        for r in range(repeats):
+            if side is not None:  # uneven load: a GEMM stream on part of the chip meanwhile
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    for _ in range(r + 1):
+                        a = (a @ a) * (1.0 / 2048)
+            got.append(run())
+        torch.cuda.synchronize()
+        assert _lib.rvq_sync_error(torch.cuda.current_stream().cuda_stream) == 0
+    finally:
+        _lib.rvq_path(prev)
+    names = ("codes", "latents", "loss_pf", "z_q_is", "z_q", "mask")
+    for g in got:
+        for name, x, y in zip(names, want, g):
+            assert (x is None and y is None) or torch.equal(x, y), name
+
+
+@pytest.mark.parametrize("nq,ncode,B,T,imp_on,zqis", [
+    (8, 1024, 32, 87, True, True),     # configs[1]: one launch of 32 clips
+    (32, 1024, 64, 87, True, True),    # configs[2]: two launches of 32 clips
+    (28, 1024, 40, 87, True, True),    # a ragged second launch
+    (5, 512, 3, 40, True, True), (1, 1024, 4, 87, False, True), (9, 256, 2, 7, True, False),
+    (2, 1024, 1, 1, True, True), (12, 768, 2, 96, True, True), (3, 1024, 5, 65, False, False),
+    (8, 1024, 3, 97, True, True)])     # T > 96: the three launches either way
+def test_rvq_fused_bit_identical_to_three_launches(nq, ncode, B, T, imp_on, zqis):
+    """The fused RVQ launch (projection units -> chain parts that publish each stage -> the
+    expansion workgroups, in-launch hand-offs) returns every output of the three launches bit
+    for bit, on repeated calls (stale flags of the previous call never pass a wait), with chain
+    parts that have no frames (T < 8), odd nq, every codebook size and the batch split over
+    launches; no wait ran out."""
+    _rvq_both_paths(nq, ncode, B, T, imp_on, zqis, 77 * nq + T + B)
+
+
+def test_rvq_fused_under_uneven_load():
+    """The fused launch while GEMMs on another stream hold part of the chip (workgroups start
+    late and unevenly): same bits as the three launches, no wait ran out."""
+    _rvq_both_paths(8, 1024, 32, 87, True, True, 4242, repeats=4, side_load=True)
+
+
+def test_rvq_fused_graph_replay():
+    """Captured in a CUDA graph (a memset of the flag block is captured before the launch):
+    replays give the three launches' bits, also after eager calls on the same stream."""
+    from vrvq_amd import _lib
+    q, gen = _random_rvq(8, 1024, 99)
+    st = q.stacked()
+    z = (torch.randn(32, 1024, 87, generator=gen) * 0.3).to(DEV)
+    imp = torch.rand(32, 87, generator=gen).to(DEV)
+    prev = _lib.rvq_path(1)
+    try:
+        want = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+        _lib.rvq_path(2)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)  # warm-up: the flag block
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+        for _ in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            for x, y in zip(want, out):
+                assert (x is None and y is None) or torch.equal(x, y)
+            eager = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+            torch.cuda.synchronize()
+            for x, y in zip(want, eager):
+                assert (x is None and y is None) or torch.equal(x, y)
+    finally:
+        _lib.rvq_path(prev)
 
 
 def test_rvq_big_batch_nq32_properties():

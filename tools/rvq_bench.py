@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
     ap.add_argument("--variants", default="2", help="projection kernel variants to time (1,2)")
+    ap.add_argument("--paths", default="2,1",
+                    help="RVQ launch structures to time (2 fused, 1 three launches)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -41,8 +43,10 @@ def main():
     run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
                                  want_z_q_is=not args.no_zqis)
     from vrvq_amd import _lib
-    for v in [int(x) for x in args.variants.split(",")]:
+    for path, v in [(int(p), int(x)) for p in args.paths.split(",")
+                    for x in args.variants.split(",")]:
         _lib.rvq_project_variant(v)
+        _lib.rvq_path(path)
         ts = []
         for it in range(args.iters):
             e0.record()
@@ -54,7 +58,7 @@ def main():
         med = sorted(ts)[len(ts) // 2]
         byt = rvq_bytes(args.batch, args.frames, args.nq)
         tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
-        print(f"projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
+        print(f"path {path} projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
               f"{med:.1f} us (min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
               f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB")
 

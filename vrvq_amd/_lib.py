@@ -73,7 +73,8 @@ SIGNATURES = {
                           _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
 }
 EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
-         "vrvq_rvq_project_variant": ([_I], _I)}
+         "vrvq_rvq_project_variant": ([_I], _I), "vrvq_rvq_path": ([_I], _I),
+         "vrvq_rvq_sync_error": ([_P, _P], _I)}
 
 _lock = threading.Lock()
 _lib = None
@@ -111,6 +112,22 @@ def call(name: str, *args) -> None:
     if rc != 0:
         msg = lib.vrvq_status_string(rc)
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else 'unknown'}")
+
+
+def rvq_path(path: int = 0) -> int:
+    """Select the RVQ launch structure (2: one fused launch where the shape allows, default; 1:
+    three launches; 0: query). Returns the previous path. Same outputs bit for bit."""
+    prev = load().vrvq_rvq_path(path)
+    if prev not in (1, 2):
+        raise RuntimeError(f"vrvq_rvq_path({path}) failed ({prev})")
+    return prev
+
+
+def rvq_sync_error(stream: int) -> int:
+    """Timeout code recorded by a fused RVQ launch on `stream` (0: none); clears it."""
+    code = ctypes.c_int(0)
+    call("vrvq_rvq_sync_error", ctypes.c_void_p(stream), ctypes.byref(code))
+    return code.value
 
 
 def rvq_project_variant(variant: int = 0) -> int:

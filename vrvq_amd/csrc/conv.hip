@@ -23,7 +23,8 @@ namespace {
 
 using namespace vrvq_conv;
 
-template <int BM, int BN, int WM, int NW, int KS, bool X3, bool PH = false>
+template <int BM, int BN, int WM, int NW, int KS, bool X3, bool PH = false,
+          bool PAIR = x3_pair<KS, BM, BN>()>
 __global__ __launch_bounds__(64 * NW)
 __attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
 void conv_mfma_kernel(ConvArgs a) {
@@ -52,7 +53,7 @@ void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TC::RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH>(a, smem, acc, b, m0, n0);
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR>(a, smem, acc, b, m0, n0);
   else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
 }
@@ -273,6 +274,38 @@ static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
   return !(ks == 1 && bm == 192 && bn == 64);
 }
 
+// The x3 launch of a tile (PAIR: its K-chunk form); VRVQ_ERR_UNSUPPORTED when its LDS does not
+// fit (the caller then takes the fp32-input loop).
+template <int BM, int BN, int WM, int NW, int KS, bool PAIR>
+int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t st) {
+  size_t lx = x3_lds_bytes<KS, BM, BN, PAIR>(XW, a.psh ? a.cin >> a.psh : a.cin);
+  if (lx < epi) lx = epi;
+  if (lx > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  if constexpr (KS == 2) {
+    if (a.psh) {  // strided conv through the phase-split view
+      if (lx > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(
+            (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
+        if (e != hipSuccess) return (int)e;
+      }
+      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR>),
+                         dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
+      return vrvq_launch_status();
+    }
+  }
+  if (a.psh) return VRVQ_ERR_ARG;
+  if (lx > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(
+        (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR>),
+                     dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
+  return vrvq_launch_status();
+}
+
 template <int BM, int BN, int WM, int NW, int KS>
 int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   ConvArgs a = a0;
@@ -293,34 +326,15 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   a.mt_slow = conv_mt_slow();
   if constexpr (NW == 4 && BM <= 192 && (KS == 1 || KS == 2 || KS == 3 || KS == 7)) {
     constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
-    size_t lx = x3_lds_bytes<KS, BM, BN>(XW, a.cin);
-    if (lx < epi) lx = epi;
-    // pair tiles (conv_x3.h) need whole K-chunks: other Cin take the fp32 loop on that tile
-    const bool pair_ok = !x3_pair<KS, BM, BN>() || a.cin % X3Cfg<KS, true>::CK == 0;
-    if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX && lx <= 160 * 1024 &&
-        x3_tile_ok(BM, BN, KS, a) && pair_ok) {
-      if constexpr (KS == 2) {
-        if (a.psh) {  // strided conv through the phase-split view
-          if (lx > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute(
-                (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
-            if (e != hipSuccess) return (int)e;
-          }
-          hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true>),
-                             dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
-          return vrvq_launch_status();
-        }
-      }
-      if (a.psh) return VRVQ_ERR_UNSUPPORTED;
-      if (lx > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
-        if (e != hipSuccess) return (int)e;
-      }
-      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true>), dim3((unsigned)nblk),
-                         dim3(64 * NW), lx, st, a);
-      return vrvq_launch_status();
+    if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX &&
+        x3_tile_ok(BM, BN, KS, a)) {
+      // pair tiles (conv_x3.h) need whole K-chunks: other Cin run the tile on plain chunks
+      int rc = VRVQ_ERR_UNSUPPORTED;
+      if (x3_pair<KS, BM, BN>() && a.cin % X3Cfg<KS, true>::CK == 0)
+        rc = launch_x3<BM, BN, WM, NW, KS, x3_pair<KS, BM, BN>()>(a, XW, epi, nblk, st);
+      else
+        rc = launch_x3<BM, BN, WM, NW, KS, false>(a, XW, epi, nblk, st);
+      if (rc != VRVQ_ERR_UNSUPPORTED) return rc;
     }
   }
   if (a.psh) return VRVQ_ERR_UNSUPPORTED;  // the phase-split view exists on the x3 loop only

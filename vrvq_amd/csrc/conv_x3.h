@@ -49,8 +49,13 @@ constexpr int x3_stages() { return BM * BN <= 128 * 128 ? 1 : 2; }
 // A pair tile needs Cin to be a multiple of the K-chunk (launch_cfg falls back otherwise). The
 // k1 + skip GEMMs on the same construction (128 x 64 tiles, two 32-channel packed chunks per
 // K-chunk) measured slower: profiles/r03_x3_pair_ab.txt.
+// The same pairing for the 2-tap GEMMs (the strided encoder convs through the phase-split view
+// and the polyphase ConvTranspose): 32-channel K-chunks of 8 octets = 4 MFMA steps (the
+// 16-channel chunk has 2), on tiles up to 128 x 128 (one LDS stage, two workgroups per CU).
 template <int KS, int BM, int BN>
-constexpr bool x3_pair() { return KS == 7 && BM == 64 && BN == 256; }
+constexpr bool x3_pair() {
+  return (KS == 7 && BM == 64 && BN == 256) || (KS == 2 && BM <= 128 && BN <= 128);
+}
 
 template <int KS, bool PAIR = false>
 struct X3Cfg {  // PAIR = false: also the HBM packing of the weight planes (vrvq_pack_x3_weight)
@@ -111,7 +116,8 @@ __device__ __forceinline__ void conv_mainloop_x3(
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
     int n0) {
   using TC = TileCfg<BM, BN, WM, NW>;
-  static_assert(!PAIR || ((KS == 7 || KS == 1) && !PH), "pair chunks: k7 / k1 stride-1 windows");
+  static_assert(!PAIR || ((KS == 7 || KS == 1) && !PH) || KS == 2,
+                "pair chunks: k7 / k1 stride-1 windows, the 2-tap GEMMs");
   using XC = X3Cfg<KS, PAIR>;
   constexpr int NO2P = X3Cfg<KS>::NO2;  // octet slots per packed (HBM) chunk
   constexpr int NOP = X3Cfg<KS>::NO;    // ... of them real (k7: 7 taps; k1: 4 channel octets)
@@ -172,7 +178,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
   // load before the chunk's MFMAs, and vmcnt retires in order, so that wait also covers the
   // W DMA issued before it: the whole memory latency exposed once per chunk.)
   // pair tiles: every input channel's Snake parameters in LDS behind the stage (their 16 per
-  // chunk do not fit the scalar registers)
+  // chunk do not fit the scalar registers); the phase-split view: per real channel (cv >> psh)
   float* snl = reinterpret_cast<float*>(sbase + X3_STAGES * STG);  // after every stage
   auto load_x = [&](int ci0) {
 #pragma unroll
@@ -237,9 +243,9 @@ __device__ __forceinline__ void conv_mainloop_x3(
             al[u] = alu[u];
             ia[u] = iau[u];
           } else if constexpr (PAIR) {  // from the LDS table (prologue)
-            const int ci = min(ci0 + c8 * 8 + u, a.cin - 1);
+            const int ci = min(ci0 + c8 * 8 + u, a.cin - 1) >> psh;
             al[u] = snl[ci];
-            ia[u] = snl[a.cin + ci];
+            ia[u] = snl[(a.cin >> psh) + ci];
           } else {
             const int ci = PH ? min(ci0 + c8 * 8 + u, a.cin - 1) >> psh : min(ci0 + c8 * 8 + u, a.cin - 1);
             al[u] = a.alpha[ci];
@@ -309,9 +315,10 @@ __device__ __forceinline__ void conv_mainloop_x3(
   };
   if constexpr (PAIR) {
     if (a.alpha != nullptr) {
-      for (int c = tid; c < a.cin; c += NT) {
+      const int nsc = a.cin >> psh;  // real channels
+      for (int c = tid; c < nsc; c += NT) {
         snl[c] = a.alpha[c];
-        snl[a.cin + c] = a.inv_alpha[c];
+        snl[nsc + c] = a.inv_alpha[c];
       }
       __syncthreads();
     }

@@ -25,6 +25,9 @@
 //
 // Codes of every golden fixture are reproduced bit for bit (the same fp32 expression for the
 // distance as the reference: dot in k order, fma(d, -2, e2) + c2, lowest index on ties).
+#include <map>
+#include <mutex>
+
 #include "common.h"
 #include "lanes.h"
 
@@ -403,8 +406,17 @@ struct ChainArgs {
                (step)] = t_;                                                               \
     }                                                                                      \
   } while (0)
+// Fused launch (rvq_fused_kernel): thread 0 of every workgroup records s_memrealtime (100 MHz,
+// one clock for the whole chip) at its phase boundaries into stamps[blockIdx][64]
+// (tools/rvq_fused_stamps.py).
+#define FSTAMP(buf, slot)                                                                    \
+  do {                                                                                     \
+    if ((buf) && threadIdx.x == 0)                                                         \
+      (buf)[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
 #else
 #define CSTAMP(stage, step) do {} while (0)
+#define FSTAMP(buf, slot) do {} while (0)
 #endif
 
 // LDS carve (floats), shared by the launcher's size computation.
@@ -475,6 +487,7 @@ struct ChainHandoff {              // fused launch only
   __amdgpu_buffer_rsrc_t zsh;      // the stage hand-off rows, stored sc1
   int zsh0;                        // float offset of (clip, stage 0, this part)
   int zsh_stage;                   // floats per stage
+  unsigned long long* stamps;      // diagnostic build only
 };
 
 template <int NM, bool FUSED>
@@ -513,6 +526,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     // (sc1) as float4: nf * R / 4 per split (R = 8 nq, the frames' rows are contiguous)
     if (wave == 0) wave_wait_ge(hx.flagp, PJ_SPLIT, hx.epoch, hx.err, 1u);
     __syncthreads();
+    FSTAMP(hx.stamps, 2);
     for (int e4 = tid; e4 < nf * R / 4; e4 += CH_NT) {
       u32x4 v[PJ_SPLIT];
 #pragma unroll
@@ -582,6 +596,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
   set_e(role ? pu_s[(rf * nq) * RCD + rk] : 0.0f);
   __syncthreads();
   CSTAMP(nq, 1);
+  if constexpr (FUSED) FSTAMP(hx.stamps, 3);
 
   // next stage's c2 slice / M column: loaded during a stage, stored to LDS at the start of the
   // next (no wait on a load issued in the same stage)
@@ -635,9 +650,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][0], b0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, d[t], 0, 0, 0);
       float bst[4];
       int bix[4];  // 16 t of the best entry (a constant per entry: no per-entry index add)
 #pragma unroll
@@ -646,8 +658,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
         bix[r] = 0;
       }
       const f32x2 m2 = {-2.0f, -2.0f}, e22 = {e2, e2};
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      auto amin_tile = [&](int t) {
         // (sum e^2 - 2 e.c) + sum c^2 with the first step as fma(d, -2, e2): 2d is exact,
         // so this is the reference's rounding (models/quantize.py:96-100); two entries per
         // packed fma / add (v_pk_fma_f32, v_pk_add_f32: the same per-element roundings)
@@ -662,7 +673,17 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
           bst[r] = take ? dist[r] : bst[r];
           bix[r] = take ? t * 16 : bix[r];
         }
+      };
+      // the second k-quad of tile t, then the argmin of tile t - 1 (whose MFMAs are done): the
+      // compare / select VALU of one tile issues while the matrix core runs the next tile
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][1], b1, d[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t > 0) amin_tile(t - 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
+      amin_tile(NT - 1);
 #pragma unroll
       for (int r = 0; r < 4; ++r) bix[r] += cw + 4 * lg + r;
       vrvq::amin(bst[0], bix[0], bst[1], bix[1]);
@@ -774,6 +795,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     CSTAMP(i, 6);
     __syncthreads();  // ------------------------------------------------- next stage's e
     CSTAMP(i, 7);
+    if constexpr (FUSED) FSTAMP(hx.stamps, 4 + i);
   }
   CSTAMP(nq, 2);
   if constexpr (FUSED) {  // publish the last stage
@@ -804,6 +826,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     }
   }
   CSTAMP(nq, 3);
+  if constexpr (FUSED) FSTAMP(hx.stamps, 36);
 }
 
 template <int NM>
@@ -909,6 +932,177 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// The fused RVQ launch (one kernel instead of projection -> chain -> expansion; T <= 96 frames
+// per clip, every workgroup of the grid resident at once). Workgroups [0, 8 B) are (clip b,
+// split / part s): the projection unit (b, s) (rvq_project2_kernel's body, partials stored
+// write-through), then chain part s of clip b (frames [s F, s F + F), F = ceil(T / 8)), which
+// waits for the clip's 8 projection units and publishes every stage's zst rows. Workgroups
+// [8 B, 16 B) are the expansion: (clip b, 128-channel block) over all stages, each stage once its
+// 8 chain parts have published it, so the z_q_is write stream runs under the chain instead of
+// after it. Same values as the three launches, bit for bit (tests/test_gpu_parity.py).
+constexpr int FU_NP = PJ_SPLIT;     // chain parts per clip
+constexpr int FU_ROWS = 16;         // frames per part block of the stage hand-off rows
+constexpr int FU_CB = 128;          // channels per expansion workgroup
+constexpr int SYNC_FLAGP = 0;       // sync block words: [clip * 32 + split]
+constexpr int SYNC_FLAGC = 1024;    //                   [clip * 32 + 2 part + wave]
+constexpr int SYNC_ERR = 2048;      //                   first timeout code (1 projection, 2 stage)
+constexpr int SYNC_WORDS = 2052;    // used words (x 4 = 8208 B, a multiple of 16)
+constexpr int FU_CLIPS_MAX = 32;    // clips per launch (flag slots)
+
+struct FusedArgs {
+  ChainArgs c;                      // part (workspace), B, T, nq, F, NF; outputs
+  const float* z;                   // [B][D][T]
+  const float* w_in_t;
+  const float* w_out;               // [nq][D][8]
+  const float* b_out;               // [nq][D]
+  float* z_q_is;                    // [B][nq][D][T] or null
+  float* z_q;                       // [B][D][T]
+  float* zsh;                       // [B][nq][FU_NP][FU_ROWS][8] stage hand-off rows
+  int zsh_bytes;
+  unsigned* sync;
+  unsigned epoch;
+  unsigned long long* stamps;       // diagnostic build only
+};
+
+// Expansion workgroup (clip b, channels [128 cb, +128)): wave w = 32-channel tile (w & 3) x
+// 32-frame tiles {w >> 2, (w >> 2) + 2}; per stage five v_mfma_f32_32x32x2_f32 per tile exactly
+// as rvq_expand_kernel (K = 10: W_out x zst, bias x 1). It waits for the stages in batches: every
+// stage the clip's parts have all published when it looks, then the next wait.
+__device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, float* sm) {
+  const int nq = f.c.nq, T = f.c.T, F = f.c.F;
+  const int b = e / (RD / FU_CB), cb = e - b * (RD / FU_CB);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = cb * FU_CB + (wave & 3) * 32;
+  const int col = lane & 31, h = lane >> 5;
+  const int n_ft = (T + 31) / 32;
+  const int ft0 = wave >> 2;
+  const bool two = ft0 + 2 < n_ft;  // wave-uniform
+  const __amdgpu_buffer_rsrc_t zr =
+      __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
+  int zoff[2];
+  int tt[2];
+  bool tv[2];
+  float sc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int t = (ft0 + 2 * j) * 32 + col;
+    tt[j] = t;
+    tv[j] = t < T && (j == 0 || two);
+    const int tc = min(t, T - 1);
+    const int p = tc / F, fr = tc - p * F;
+    zoff[j] = ((b * nq * FU_NP + p) * FU_ROWS + fr) * RCD;  // stage 0
+    sc[j] = (f.c.imp && tv[j]) ? (f.c.imp[(size_t)b * T + tc] * f.c.level) * (float)nq : INFINITY;
+  }
+  const int zstage = FU_NP * FU_ROWS * RCD;
+  const int cr = c0 + col;  // A-operand row of this lane
+  const float* wp = f.w_out + (size_t)cr * RCD;
+  const size_t wstride = (size_t)RD * RCD;
+  f32x16 zq[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) zq[j][r] = 0.0f;
+  unsigned* avail_s = reinterpret_cast<unsigned*>(sm);  // [2]: alternating broadcast words
+  const unsigned base = f.epoch * 64u;
+  bool dead = false;
+  int i = 0;
+  for (int it = 0; i < nq; ++it) {
+    if (wave == 0) {
+      unsigned v = dead ? 0u
+                        : wave_wait_ge(f.sync + SYNC_FLAGC + b * 32, 2 * FU_NP, base + i + 1,
+                                       f.sync + SYNC_ERR, 2u);
+      if (lane == 0) avail_s[it & 1] = v ? v - base : (unsigned)nq;  // timeout: run on
+    }
+    __syncthreads();
+    const int upto = min((int)avail_s[it & 1], nq);
+    dead = dead || upto <= i;  // a wait ran out: no more waits
+    for (; i < upto; ++i) {
+      FSTAMP(f.stamps, 1 + i);
+      const float4 w0 = ld4(wp + i * wstride), w1 = ld4(wp + i * wstride + 4);
+      const float bb = f.b_out[(size_t)i * RD + cr];
+      const float wa[4] = {h ? w0.y : w0.x, h ? w0.w : w0.z, h ? w1.y : w1.x, h ? w1.w : w1.z};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j == 1 && !two) break;
+        const int off = (zoff[j] + i * zstage) * 4;
+        const u32x4 z0 = __builtin_amdgcn_raw_buffer_load_b128(zr, off, 0, CPOL_SC1);
+        const u32x4 z1 = __builtin_amdgcn_raw_buffer_load_b128(zr, off + 16, 0, CPOL_SC1);
+        const float zb[4] = {__uint_as_float(h ? z0[1] : z0[0]), __uint_as_float(h ? z0[3] : z0[2]),
+                             __uint_as_float(h ? z1[1] : z1[0]), __uint_as_float(h ? z1[3] : z1[2])};
+        f32x16 q;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) q[r] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : bb, h ? 0.0f : 1.0f, q, 0, 0, 0);
+        const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
+        if (f.z_q_is && tv[j]) {
+          float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = q[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) zq[j][r] = zq[j][r] + q[r] * m;
+      }
+    }
+  }
+  FSTAMP(f.stamps, 40);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (tv[j]) {
+      float* dst = f.z_q + ((size_t)b * RD + c0 + 4 * h) * T + tt[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = zq[j][r];
+    }
+  }
+}
+
+template <int NM>
+__global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = f.c.B, T = f.c.T, nq = f.c.nq, F = f.c.F;
+  const int blk = blockIdx.x;
+  FSTAMP(f.stamps, 0);
+  if (blk >= B * FU_NP) {
+    fused_expand_body(f, blk - B * FU_NP, sm);
+    FSTAMP(f.stamps, 41);
+    return;
+  }
+  const int b = blk / FU_NP, s = blk - b * FU_NP;
+  const int R = nq * RCD;
+  float* part = const_cast<float*>(f.c.part);  // the workspace this launch writes
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+      part, (short)0, (int)((size_t)PJ_SPLIT * f.c.NF * R * 4), RSRC_FLAGS);
+  // projection unit (b, s): partials write-through, every storing wave drained, one flag
+  PartSink out{part, pr, true};
+  project2_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, sm);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  FSTAMP(f.stamps, 1);
+  if (threadIdx.x == 0) st_flag(f.sync + SYNC_FLAGP + b * 32 + s, f.epoch);
+  // chain part s of clip b
+  const int nf = min(F, T - s * F);
+  unsigned* flagc = f.sync + SYNC_FLAGC + b * 32 + 2 * s;
+  if (nf <= 0) {  // no frames (T < 8 F): nothing to publish but the count
+    if (threadIdx.x < 2) st_flag(flagc + threadIdx.x, f.epoch * 64u + (unsigned)nq);
+    return;
+  }
+  ChainHandoff hx;
+  hx.flagp = f.sync + SYNC_FLAGP + b * 32;
+  hx.flagc = flagc;
+  hx.err = f.sync + SYNC_ERR;
+  hx.epoch = f.epoch;
+  hx.part = pr;
+  hx.zsh = __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
+  hx.zsh0 = (b * nq * FU_NP + s) * FU_ROWS * RCD;
+  hx.zsh_stage = FU_NP * FU_ROWS * RCD;
+  hx.stamps = f.stamps;
+  chain_body<NM, true>(f.c, sm, b * T + s * F, nf, hx);
+}
+
+// ------------------------------------------------------------------------------------------
 // Projection kernel: 2 = rvq_project2_kernel (one workgroup per clip x split, default), 1 =
 // rvq_project_kernel (48-frame tiles x 64-row blocks). Same partials bit for bit (A/B timing and
 // the bit-identity test; VRVQ_RVQ_PROJECT=1 in the environment).
@@ -946,7 +1140,8 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
   return vrvq_launch_status();
 }
 
-unsigned long long* g_stamps = nullptr;  // diagnostic build: vrvq_debug_set_stamps
+unsigned long long* g_stamps = nullptr;   // diagnostic build: vrvq_debug_set_stamps
+unsigned long long* g_fstamps = nullptr;  // diagnostic build: vrvq_debug_set_fused_stamps
 
 template <int NM>
 int launch_chain_nm(const ChainArgs& a, hipStream_t st, long long nblk) {
@@ -1001,12 +1196,158 @@ bool rvq_shape_ok(int dim, int cdim, int nq, int ncode) {
 
 size_t part_floats(long long nf, int nq) { return (size_t)PJ_SPLIT * nf * nq * RCD; }
 
+// zst rows of the three-launch path ([B][nq][T][8]) or the fused path's stage hand-off rows
+// ([B][nq][FU_NP][FU_ROWS][8]): the workspace holds the larger
+size_t zst_floats(int batch, int frames, int nq) {
+  const size_t a = (size_t)batch * frames * nq * RCD;
+  const size_t b = (size_t)batch * nq * FU_NP * FU_ROWS * RCD;
+  return a > b ? a : b;
+}
+
+// ---- fused path, host side -----------------------------------------------------------------
+// 1: three launches everywhere; 2: the fused launch where the shape allows (default;
+// VRVQ_RVQ_FUSED=0 in the environment or vrvq_rvq_path(1) for the A/B).
+int g_rvq_path = 0;
+
+int rvq_path() {
+  if (g_rvq_path == 0) {
+    const char* e = getenv("VRVQ_RVQ_FUSED");
+    g_rvq_path = (e && e[0] == '0') ? 1 : 2;
+  }
+  return g_rvq_path;
+}
+
+// Per (device, stream): the flag block the fused launches on that stream share (serialised by
+// the stream) and the last epoch used. Eager calls take epochs 2, 3, ...: every flag an older
+// call left is below this call's targets. Under stream capture the graph gets a memset node of
+// the block before the kernel and epoch 1, so every replay starts from zeros.
+struct SyncBlock {
+  unsigned* dev = nullptr;
+  unsigned epoch = 1;
+};
+std::mutex g_sync_mu;
+std::map<std::pair<int, hipStream_t>, SyncBlock> g_sync;
+constexpr unsigned EPOCH_RESET = 1u << 24;  // 64 epoch + stage stays below 2^32
+
+bool sync_for_launch(hipStream_t st, unsigned** dev, unsigned* epoch) {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  std::lock_guard<std::mutex> guard(g_sync_mu);
+  SyncBlock& sb = g_sync[{device, st}];
+  const size_t bytes = SYNC_WORDS * sizeof(unsigned);
+  if (!sb.dev) {
+    if (capturing) return false;  // no allocation inside a capture: three launches this time
+    if (hipMalloc(&sb.dev, bytes) != hipSuccess) {
+      sb.dev = nullptr;
+      return false;
+    }
+    if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
+  }
+  if (capturing) {
+    if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
+    *epoch = 1;
+  } else {
+    if (++sb.epoch >= EPOCH_RESET) {
+      if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
+      sb.epoch = 2;
+    }
+    *epoch = sb.epoch;
+  }
+  *dev = sb.dev;
+  return true;
+}
+
+// Clips per fused launch: every workgroup (2 per clip and part) resident at once, so that no
+// waiting workgroup can hold the slot of one it waits for (occupancy query, cached).
+template <int NM>
+int fused_clip_capacity(size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, size_t>, int> cache;
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> guard(mu);
+  auto it = cache.find({device, lds});
+  if (it != cache.end()) return it->second;
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rvq_fused_kernel<NM>, CH_NT, lds) !=
+          hipSuccess)
+    cus = per = 0;
+  const int clips = min(FU_CLIPS_MAX, cus * per / (2 * FU_NP));
+  cache[{device, lds}] = clips;
+  return clips;
+}
+
+constexpr int FUSED_NA = -1;  // the fused launch does not apply: take the three launches
+
+template <int NM>
+int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* z,
+                    const float* imp, int64_t* codes, float* latents, float* loss_pf,
+                    float* z_q_is, float* z_q, float* mask, float* ws, hipStream_t st) {
+  const int F = (frames + FU_NP - 1) / FU_NP;
+  size_t lds = (size_t)ChainLds(nq, F, 256 * NM).total * sizeof(float);
+  const size_t lds_pj = (size_t)PJ_CPS * PJ2_LD * sizeof(float);
+  if (lds < lds_pj) lds = lds_pj;
+  if (lds > 80 * 1024) return FUSED_NA;
+  const int cap = fused_clip_capacity<NM>(lds);
+  if (cap < 1) return FUSED_NA;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_fused_kernel<NM>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const int bc_max = min(batch, cap);
+  float* part = ws;
+  float* zsh = ws + part_floats((long long)bc_max * frames, nq);
+  const size_t DT = (size_t)RD * frames;
+  for (int b0 = 0; b0 < batch; b0 += bc_max) {
+    const int bc = min(bc_max, batch - b0);
+    FusedArgs f = f0;
+    if (!sync_for_launch(st, &f.sync, &f.epoch)) {
+      if (b0 == 0) return FUSED_NA;
+      return VRVQ_ERR_UNSUPPORTED;  // cannot happen after a first successful chunk
+    }
+    ChainArgs& c = f.c;
+    c.part = part;
+    c.B = bc;
+    c.T = frames;
+    c.nq = nq;
+    c.F = F;
+    c.NF = bc * frames;
+    c.imp = imp ? imp + (size_t)b0 * frames : nullptr;
+    c.codes = codes + (size_t)b0 * nq * frames;
+    c.latents = latents + (size_t)b0 * nq * RCD * frames;
+    c.loss_pf = loss_pf + (size_t)b0 * nq * frames;
+    c.zst = nullptr;
+    c.mask = mask ? mask + (size_t)b0 * nq * frames : nullptr;
+    c.stamps = nullptr;
+    f.z = z + b0 * DT;
+    f.z_q_is = z_q_is ? z_q_is + (size_t)b0 * nq * DT : nullptr;
+    f.z_q = z_q + b0 * DT;
+    f.zsh = zsh;
+    f.zsh_bytes = (int)((size_t)bc * nq * FU_NP * FU_ROWS * RCD * sizeof(float));
+    f.stamps = g_fstamps;
+    hipLaunchKernelGGL(rvq_fused_kernel<NM>, dim3((unsigned)(2 * bc * FU_NP)), dim3(CH_NT), lds, st,
+                       f);
+    const int rc = vrvq_launch_status();
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 }  // namespace
 
 #ifdef VRVQ_STAMPS
 // Diagnostic build only (not in include/vrvq.h): the chain kernel's stamp buffer.
 extern "C" int vrvq_debug_set_stamps(unsigned long long* buf) {
   g_stamps = buf;
+  return 0;
+}
+extern "C" int vrvq_debug_set_fused_stamps(unsigned long long* buf) {
+  g_fstamps = buf;
   return 0;
 }
 #endif
@@ -1092,7 +1433,37 @@ extern "C" int vrvq_rvq_expand_masked(const float* zst, int batch, int dim, int 
 extern "C" int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes) {
   VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0);
   const long long nf = (long long)batch * frames;
-  *bytes = (long long)(part_floats(nf, nq) + (size_t)nf * nq * RCD) * (long long)sizeof(float);
+  *bytes = (long long)(part_floats(nf, nq) + zst_floats(batch, frames, nq)) *
+           (long long)sizeof(float);
+  return 0;
+}
+
+extern "C" int vrvq_rvq_path(int path) {
+  const int prev = rvq_path();
+  if (path == 1 || path == 2) g_rvq_path = path;
+  else if (path != 0) return VRVQ_ERR_ARG;
+  return prev;
+}
+
+extern "C" int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code) {
+  VRVQ_CHECK_ARG(code);
+  *code = 0;
+  hipStream_t st = as_stream(stream);
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return VRVQ_ERR_ARG;
+  unsigned* dev = nullptr;
+  {
+    std::lock_guard<std::mutex> guard(g_sync_mu);
+    auto it = g_sync.find({device, st});
+    if (it == g_sync.end() || !it->second.dev) return 0;
+    dev = it->second.dev;
+  }
+  unsigned v = 0;
+  hipError_t e = hipMemcpyAsync(&v, dev + SYNC_ERR, sizeof(v), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && v) e = hipMemsetAsync(dev + SYNC_ERR, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) return (int)e;
+  *code = (int)v;
   return 0;
 }
 
@@ -1116,6 +1487,23 @@ extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, i
   float* part = static_cast<float*>(workspace);
   float* zst = part + part_floats(nf, nq);
   hipStream_t st = as_stream(stream);
+  if (rvq_path() == 2 && frames <= PJ2_TC && batch <= 0x7fffffff / (2 * FU_NP)) {
+    FusedArgs f{};
+    ChainArgs& c = f.c;
+    c.b_in = b_in; c.qb = qb; c.mcol = mcol; c.cb = cb; c.cbf = cbf; c.c2 = c2;
+    c.level = level;
+    f.w_in_t = w_in_t;
+    f.w_out = w_out;
+    f.b_out = b_out;
+    int rc = FUSED_NA;
+    switch (ncode / 256) {
+      case 1: rc = launch_fused_nm<1>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
+      case 2: rc = launch_fused_nm<2>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
+      case 3: rc = launch_fused_nm<3>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
+      default: rc = launch_fused_nm<4>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
+    }
+    if (rc != FUSED_NA) return rc;
+  }
   int rc = launch_project(z, batch, frames, nq, w_in_t, part, st);
   if (rc) return rc;
   rc = vrvq_rvq_chain(part, batch, frames, nq, ncode, cdim, b_in, qb, mcol, cb, cbf, c2, imp,
