@@ -13,8 +13,8 @@ Multi-GPU: clips shard data-parallel (each rank its own clips, no data-path coll
 scaling; the timed region is bracketed by barrier + synchronize and the MAX over ranks is
 reported; the sweep's [audio seconds, bits, frames] are SUM-reduced over ranks (RCCL) so its
 bpf / kbps are job-wide. Rank 0 prints one JSON line, including
-  roofline      the RVQ path (torch.ops.vrvq.rvq_encode: projection -> chain -> expansion)
-                against HBM, bytes per SURVEY.md §8(d), per-launch durations from HIP events
+  roofline      the RVQ path (torch.ops.vrvq.rvq_encode: one fused launch of projection ->
+                chain -> expansion) against HBM, bytes per SURVEY.md §8(d), per-launch durations from HIP events
                 recorded on the launch stream inside the timed steps; per-kernel split from the
                 committed rocprofv3 summary; traffic from the committed PMC passes;
   roofline_conv the conv stacks (fp32 arithmetic: the x3 split-bf16 MFMA path for stride-1
@@ -48,7 +48,8 @@ X3_PEAK_TFLOPS = 2516.6 / 6    # fp32 FLOPs on the bf16 MFMA with the exact 3-wa
 CLIP_SAMPLES = 44100
 SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
-RVQ_KERNELS = ("rvq_project2_kernel", "rvq_chain_kernel", "rvq_expand_kernel")
+RVQ_KERNELS = ("rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
+               "rvq_chain_kernel", "rvq_expand_kernel")
 
 
 def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024) -> int:
@@ -139,8 +140,8 @@ def conv_flops(model, B: int, L: int):
 
 
 class RvqTimer:
-    """HIP-event timing of the RVQ operator (torch.ops.vrvq.rvq_encode: three launches),
-    recorded on the stream it runs on."""
+    """HIP-event timing of the RVQ operator (torch.ops.vrvq.rvq_encode: one fused launch at
+    these shapes), recorded on the stream it runs on."""
 
     def __init__(self):
         self.events = []
@@ -451,8 +452,9 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "RVQ path: rvq_project2_kernel -> rvq_chain_kernel -> "
-                                   "rvq_expand_kernel (one torch.ops.vrvq.rvq_encode)",
+                         "kernel": "RVQ path: one torch.ops.vrvq.rvq_encode = ONE launch of "
+                                   "rvq_fused_kernel (projection units -> chain parts -> "
+                                   "expansion workgroups, in-launch hand-offs) at T <= 96",
                          "bytes_per_launch": byt, "path_us": round(rvq_ms * 1e3, 2),
                          "kernel_us_rocprof": split, "kernel_us_source": split_src},
             "roofline_conv": {"bound": "mfma", "achieved": round(conv_tflops, 2),

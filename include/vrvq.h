@@ -210,11 +210,13 @@ int vrvq_rvq_cross_prep(const float* w_in_t, const float* w_out, const float* b_
 int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
                   vrvq_stream_t stream);
 
-/* Projection kernel used by vrvq_rvq_project / vrvq_rvq_encode (process-wide): 2 = one
- * workgroup per clip x channel split, z slab staged once in LDS (default); 1 = 48-frame tiles x
- * 64-row blocks. Both write the same partials bit for bit (A/B timing, bit-identity test; also
- * VRVQ_RVQ_PROJECT=1 in the environment). variant 0 queries. Returns the previous variant (1 or
- * 2), or VRVQ_ERR_ARG. */
+/* Projection kernel used by vrvq_rvq_project / vrvq_rvq_encode (both launch structures,
+ * process-wide): 3 = one workgroup per clip x channel split on the bf16 matrix cores with both
+ * operands split exactly into three bf16 terms (six products, fp32 accuracy; default); 2 = the
+ * same unit on the fp32-input MFMA; 1 = 48-frame tiles x 64-row blocks (fp32). 1 and 2 write the
+ * same partials bit for bit; 3 agrees with them to fp32 rounding (A/B timing; also
+ * VRVQ_RVQ_PROJECT=1 / 2 in the environment). variant 0 queries. Returns the previous variant
+ * (1, 2 or 3), or VRVQ_ERR_ARG. */
 int vrvq_rvq_project_variant(int variant);
 
 /* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows /

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
-    ap.add_argument("--variants", default="2", help="projection kernel variants to time (1,2)")
+    ap.add_argument("--variants", default="3,2", help="projection kernel variants to time (1,2,3)")
     ap.add_argument("--paths", default="2,1",
                     help="RVQ launch structures to time (2 fused, 1 three launches)")
     args = ap.parse_args()
@@ -56,11 +56,20 @@ def main():
             if it >= min(5, args.iters - 1):
                 ts.append(e0.elapsed_time(e1) * 1e3)
         med = sorted(ts)[len(ts) // 2]
+        # back to back: the host enqueues ahead of the GPU, as inside bench.py's step
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        b2b = e0.elapsed_time(e1) * 1e3 / args.iters
         byt = rvq_bytes(args.batch, args.frames, args.nq)
         tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
         print(f"path {path} projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
               f"{med:.1f} us (min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
-              f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB")
+              f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB; back to back "
+              f"{b2b:.1f} us/call ({byt / b2b / 1e3 / 8000:.3f})")
 
 
 if __name__ == "__main__":

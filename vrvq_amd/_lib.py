@@ -131,9 +131,10 @@ def rvq_sync_error(stream: int) -> int:
 
 
 def rvq_project_variant(variant: int = 0) -> int:
-    """Select the RVQ projection kernel (2: clip x split workgroups, default; 1: 48-frame tiles;
-    0: query). Returns the previous variant. Both write the same bits (tests/test_gpu_parity.py)."""
+    """Select the RVQ projection kernel (3: clip x split workgroups on the split-bf16 MFMA,
+    default; 2: the same on the fp32 MFMA; 1: 48-frame tiles; 0: query). Returns the previous
+    variant. 1 and 2 write the same bits (tests/test_gpu_parity.py)."""
     prev = load().vrvq_rvq_project_variant(variant)
-    if prev not in (1, 2):
+    if prev not in (1, 2, 3):
         raise RuntimeError(f"vrvq_rvq_project_variant({variant}) failed ({prev})")
     return prev

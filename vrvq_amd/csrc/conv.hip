@@ -217,6 +217,72 @@ __global__ __launch_bounds__(256) void conv_cout1_stream_kernel(ConvArgs a) {
   }
 }
 
+// Cin = 1 conv (the encoder's 1 -> 64 k7 input conv, models/dac_vrvq.py:27): no MFMA tile
+// (K = 7), HBM-bound on writing y and snake(y) (2 x 64 x 4 B per sample). Thread = 4
+// consecutive output samples x CI1_CG channels; its 4 + KS - 1 input samples once, per channel
+// the k-ordered fmaf chain from 0, then conv_epilogue's expressions (bias, residual, act, the
+// next layer's Snake) and one 16-B store per output row: a wave writes 1 KB runs per channel.
+constexpr int CI1_T = 4;
+constexpr int CI1_CG = 16;
+template <int KS>
+__global__ __launch_bounds__(256) void conv_cin1_stream_kernel(ConvArgs a) {
+  const int n_t = (a.ng + 256 * CI1_T - 1) / (256 * CI1_T);
+  const int n_cg = a.M / CI1_CG;
+  int blk = blockIdx.x;
+  const int cg = blk % n_cg;
+  blk /= n_cg;
+  const int tt = blk % n_t, b = blk / n_t;
+  const int t0 = (tt * 256 + (int)threadIdx.x) * CI1_T;
+  if (t0 >= a.ng) return;  // no barrier in this kernel
+  const float* xb = a.x + (size_t)b * a.tin;
+  constexpr int W = CI1_T + KS - 1;
+  float xv[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {  // clamped address, zeroed outside [0, tin) (zero padding)
+    const int t = t0 - a.pad + j;
+    const float v = xb[min(max(t, 0), a.tin - 1)];
+    xv[j] = __uint_as_float(__float_as_uint(v) & (0u - (unsigned)(t >= 0 && t < a.tin)));
+  }
+  const bool full = t0 + CI1_T <= a.ng;
+#pragma unroll 4
+  for (int c = 0; c < CI1_CG; ++c) {
+    const int co = cg * CI1_CG + c;
+    float v[CI1_T];
+#pragma unroll
+    for (int u = 0; u < CI1_T; ++u) v[u] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const float wv = a.w[(size_t)k * a.m_pad + co];
+#pragma unroll
+      for (int u = 0; u < CI1_T; ++u) v[u] = fmaf(wv, xv[k + u], v[u]);
+    }
+    const float bb = a.bias ? a.bias[co] : 0.0f;
+    const size_t o = ((size_t)b * a.cout + co) * a.ylen + t0;
+#pragma unroll
+    for (int u = 0; u < CI1_T; ++u) v[u] = v[u] + bb;
+    if (a.res) {
+#pragma unroll
+      for (int u = 0; u < CI1_T; ++u)
+        if (full || t0 + u < a.ng) v[u] = a.res[o + u] + v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < CI1_T; ++u) v[u] = apply_epi(v[u], a.epi);
+    if (a.y) {
+      if (full) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+      else
+        for (int u = 0; u < CI1_T; ++u)
+          if (t0 + u < a.ng) a.y[o + u] = v[u];
+    }
+    if (a.ys) {
+      snake_n1<CI1_T>(v, a.alpha_o[co], a.inv_alpha_o[co]);
+      if (full) *reinterpret_cast<float4*>(a.ys + o) = make_float4(v[0], v[1], v[2], v[3]);
+      else
+        for (int u = 0; u < CI1_T; ++u)
+          if (t0 + u < a.ng) a.ys[o + u] = v[u];
+    }
+  }
+}
+
 int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
   if (a.M == 1 && a.cout == 1 && a.stride == 1 && a.dil == 1 && a.tin % 4 == 0 &&
       ((ks == 7 && a.pad == 3) || (ks == 3 && a.pad == 1))) {
@@ -244,6 +310,25 @@ int launch_small(const ConvArgs& a, int batch, int ks, hipStream_t st) {
   else
     hipLaunchKernelGGL(conv_small_cout_kernel<SMALL_COUT>, dim3((unsigned)nblk), dim3(256), lds, st, a, ks);
   return vrvq_launch_status();
+}
+
+// x3 ConvTranspose with M a multiple of 96 (not of 128): 96-row pair tiles (default) |
+// VRVQ_CONV_CONVT96=0: the 192 x 128 two-stage tile
+static int convt_96() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_CONVT96");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// Cin = 1 convs on conv_cin1_stream_kernel (default) | VRVQ_CONV_CIN1=0: the fp32 MFMA tile
+static int cin1_stream() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_CIN1");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 // tuning override: VRVQ_CONV_MTSLOW=1 (M tile slowest) | 0 (default: 495.1 vs 492.6
@@ -483,6 +568,12 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     if (bn == 64) return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
+  if (KS == 2 && a.up > 0 && a.w3 != nullptr && a.M % 96 == 0 && a.M % 128 != 0 &&
+      convt_96()) {
+    // x3 polyphase ConvTranspose1d with 96-row multiples (192 -> 96 s2: M = 192): 96-row
+    // tiles on the pair chunks (two workgroups per CU) instead of the two-stage 192 x 128 tile
+    return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
+  }
   if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
     // (KS == 2 with up > 0: the polyphase ConvTranspose1d 192->96 s2, M = 192 phase rows)
     if constexpr (kWide) if (wide) return launch_cfg<192, 256, 2, 8, KS>(a, batch, st);
@@ -658,6 +749,15 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   }
   if (cout <= SMALL_COUT && stride == 1 && cin * k * (cout == 1 ? 1 : SMALL_COUT) <= SMALL_WMAX)
     return launch_small(a, batch, k, as_stream(stream));
+  if (cin == 1 && k == 7 && stride == 1 && dil == 1 && !alpha && cout % CI1_CG == 0 &&
+      tout % 4 == 0 && cin1_stream()) {
+    const long long nblk =
+        (long long)batch * ((tout + 256 * CI1_T - 1) / (256 * CI1_T)) * (cout / CI1_CG);
+    if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+    hipLaunchKernelGGL(conv_cin1_stream_kernel<7>, dim3((unsigned)nblk), dim3(256), 0,
+                       as_stream(stream), a);
+    return vrvq_launch_status();
+  }
   return dispatch_ks(k, a, batch, as_stream(stream));
 }
 

@@ -358,6 +358,145 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __res
 }
 
 // ------------------------------------------------------------------------------------------
+// Projection on the bf16 matrix cores (variant 3): the same unit as rvq_project2_kernel (clip,
+// <= 96-frame tile, 128-channel split), with both operands split exactly into three bf16 terms
+// and the six products of conv_x3.h (dropped terms <= 2^-23 |ab|: fp32 accuracy) on
+// v_mfma_f32_16x16x32_bf16 -- 2.7x the fp32 MFMA rate for the GEMM that bounds the projection
+// (64 rows x 128 channels x 96 frames per unit). The z slab goes to LDS transposed, as three
+// bf16 planes [plane][frame][channel] (rows of 128 channels + 8 pad: conflict-free 16-B B
+// reads); the W_in rows (8 channels per lane, L2) are split in registers.
+constexpr int PJ3_LDB = 136;                     // bf16 per frame row (272 B)
+constexpr int PJ3_PLANE = PJ2_TC * PJ3_LDB * 2;  // bytes per plane
+constexpr int PJ3_LDS = 3 * PJ3_PLANE;           // 78,336 B
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// v = h + m + l exactly (RNE at each step), two values per call (conv_x3.h split3x2)
+__device__ __forceinline__ void rvq_split3x2(float v0, float v1, unsigned& h, unsigned& m,
+                                             unsigned& l) {
+  const f32x2 v = {v0, v1};
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+  const f32x2 hf = {__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+  const f32x2 r = v - hf;
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+  const f32x2 mf = {__uint_as_float(mu << 16), __uint_as_float(mu & 0xffff0000u)};
+  const f32x2 s = r - mf;
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2));
+}
+
+__device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void project3_body(const float* __restrict__ z, int T, int nq, int tc,
+                                              int b, int s, const float* __restrict__ w_in_t,
+                                              const PartSink& out, int NF, char* lds) {
+  constexpr int NIT = (PJ_CPS / 8) * PJ2_TC / PJ2_NT;  // (octet, frame) items per thread: 3
+  const int R = nq * RCD;
+  const int t0 = tc * PJ2_TC;
+  const int ntl = min(PJ2_TC, T - t0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
+  {  // the slab: every load in flight, then split and stored transposed
+    float zv[NIT][8];
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) {
+      const int e = tid + PJ2_NT * q;
+      const int o = e / PJ2_TC, t = e - o * PJ2_TC;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zv[q][u] = zb[(size_t)(8 * o + u) * T + min(t, ntl - 1)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NIT; ++q) {
+      const int e = tid + PJ2_NT * q;
+      const int o = e / PJ2_TC, t = e - o * PJ2_TC;
+      const unsigned m = 0u - (unsigned)(t < ntl);
+      unsigned h[4], mm[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        rvq_split3x2(__uint_as_float(__float_as_uint(zv[q][2 * u]) & m),
+                     __uint_as_float(__float_as_uint(zv[q][2 * u + 1]) & m), h[u], mm[u], l[u]);
+      char* d = lds + t * (PJ3_LDB * 2) + o * 16;
+      *reinterpret_cast<u32x4*>(d) = u32x4{h[0], h[1], h[2], h[3]};
+      *reinterpret_cast<u32x4*>(d + PJ3_PLANE) = u32x4{mm[0], mm[1], mm[2], mm[3]};
+      *reinterpret_cast<u32x4*>(d + 2 * PJ3_PLANE) = u32x4{l[0], l[1], l[2], l[3]};
+    }
+  }
+  __syncthreads();
+  // work items (16-row tile rt, half hf = frame tiles 3 hf .. 3 hf + 2) over the 8 waves
+  const int n_rt = (R + 15) / 16;
+  const int lr = lane & 15, kg = lane >> 4;
+  for (int item = wave; item < 2 * n_rt; item += PJ2_NT / 64) {
+    const int rt = item >> 1, hf = item & 1;
+    // A: row r = 16 rt + lr, channels 32 ks + 8 kg .. +7 of the split (w_in_t[stage][c][k])
+    const int r = rt * 16 + lr;
+    const unsigned rm = 0u - (unsigned)(r < R);
+    const float* wp = w_in_t + ((size_t)min(r >> 3, nq - 1) * RD + s * PJ_CPS + 8 * kg) * RCD + (r & 7);
+    float wn[8];  // the next K step's 8 weights in flight while this step's MFMAs run
+#pragma unroll
+    for (int u = 0; u < 8; ++u) wn[u] = __uint_as_float(__float_as_uint(wp[(size_t)u * RCD]) & rm);
+    f32x4 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < PJ_CPS / 32; ++ks) {
+      unsigned h[4], mm[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rvq_split3x2(wn[2 * u], wn[2 * u + 1], h[u], mm[u], l[u]);
+      const u32x4 ah = {h[0], h[1], h[2], h[3]}, am = {mm[0], mm[1], mm[2], mm[3]},
+                  al = {l[0], l[1], l[2], l[3]};
+      if (ks + 1 < PJ_CPS / 32) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          wn[u] = __uint_as_float(__float_as_uint(wp[(size_t)(32 * (ks + 1) + u) * RCD]) & rm);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const char* bp = lds + ((3 * hf + j) * 16 + lr) * (PJ3_LDB * 2) + (32 * ks + 8 * kg) * 2;
+        const u32x4 bh = *reinterpret_cast<const u32x4*>(bp);
+        const u32x4 bm = *reinterpret_cast<const u32x4*>(bp + PJ3_PLANE);
+        const u32x4 bl = *reinterpret_cast<const u32x4*>(bp + 2 * PJ3_PLANE);
+        __builtin_amdgcn_sched_barrier(0);  // one tile's operands live at a time
+        f32x4 c = acc[j];
+        c = mfma16_bf16(am, bm, c);  // m m
+        c = mfma16_bf16(ah, bl, c);  // h l
+        c = mfma16_bf16(al, bh, c);  // l h
+        c = mfma16_bf16(ah, bm, c);  // h m
+        c = mfma16_bf16(am, bh, c);  // m h
+        acc[j] = mfma16_bf16(ah, bh, c);  // h h
+      }
+    }
+    // D layout: lane l, reg q -> row 4 (l >> 4) + q of the tile, frame l & 15
+    const int rr = rt * 16 + 4 * kg;  // rows rr..rr+3 all valid iff rr < R (R = 8 nq)
+    if (rr < R) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int t = (3 * hf + j) * 16 + lr;
+        if (t < ntl) {
+          const size_t n = (size_t)b * T + t0 + t;
+          out.put(((size_t)s * NF + n) * R + rr, make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]));
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(PJ2_NT) void rvq_project3_kernel(const float* __restrict__ z, int T,
+                                                              int nq, int n_tc,
+                                                              const float* __restrict__ w_in_t,
+                                                              float* __restrict__ part, int NF) {
+  extern __shared__ __attribute__((aligned(16))) char lds3[];
+  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), false};
+  project3_body(z, T, nq, blockIdx.x % n_tc, blockIdx.x / n_tc, blockIdx.y, w_in_t, out, NF, lds3);
+}
+
+// ------------------------------------------------------------------------------------------
 // The chain. Workgroup = frames [n0, n0 + nf) of the flattened (b, t) axis, nf <= 16; 8 waves.
 //
 // Stage i, S1 (all waves):
@@ -1059,7 +1198,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   }
 }
 
-template <int NM>
+template <int NM, bool PJ3>
 __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int B = f.c.B, T = f.c.T, nq = f.c.nq, F = f.c.F;
@@ -1077,7 +1216,8 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
       part, (short)0, (int)((size_t)PJ_SPLIT * f.c.NF * R * 4), RSRC_FLAGS);
   // projection unit (b, s): partials write-through, every storing wave drained, one flag
   PartSink out{part, pr, true};
-  project2_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, sm);
+  if constexpr (PJ3) project3_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, reinterpret_cast<char*>(sm));
+  else project2_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, sm);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   FSTAMP(f.stamps, 1);
@@ -1111,7 +1251,7 @@ int g_project_variant = 0;  // 0: not yet read from the environment
 int project_variant() {
   if (g_project_variant == 0) {
     const char* e = getenv("VRVQ_RVQ_PROJECT");
-    g_project_variant = (e && e[0] == '1') ? 1 : 2;
+    g_project_variant = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
   }
   return g_project_variant;
 }
@@ -1120,6 +1260,16 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
                    float* part, hipStream_t st) {
   const long long nf = (long long)batch * frames;
   VRVQ_CHECK_ARG(nf * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
+  if (project_variant() == 3) {
+    const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
+    VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_project3_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, PJ3_LDS);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(rvq_project3_kernel, dim3((unsigned)(batch * n_tc), PJ_SPLIT), dim3(PJ2_NT),
+                       PJ3_LDS, st, z, frames, nq, n_tc, w_in_t, part, (int)nf);
+    return vrvq_launch_status();
+  }
   if (project_variant() == 2) {
     const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
     VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
@@ -1262,7 +1412,7 @@ bool sync_for_launch(hipStream_t st, unsigned** dev, unsigned* epoch) {
 
 // Clips per fused launch: every workgroup (2 per clip and part) resident at once, so that no
 // waiting workgroup can hold the slot of one it waits for (occupancy query, cached).
-template <int NM>
+template <int NM, bool PJ3>
 int fused_clip_capacity(size_t lds) {
   static std::mutex mu;
   static std::map<std::pair<int, size_t>, int> cache;
@@ -1273,7 +1423,7 @@ int fused_clip_capacity(size_t lds) {
   if (it != cache.end()) return it->second;
   int cus = 0, per = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rvq_fused_kernel<NM>, CH_NT, lds) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rvq_fused_kernel<NM, PJ3>, CH_NT, lds) !=
           hipSuccess)
     cus = per = 0;
   const int clips = min(FU_CLIPS_MAX, cus * per / (2 * FU_NP));
@@ -1283,19 +1433,19 @@ int fused_clip_capacity(size_t lds) {
 
 constexpr int FUSED_NA = -1;  // the fused launch does not apply: take the three launches
 
-template <int NM>
+template <int NM, bool PJ3>
 int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* z,
                     const float* imp, int64_t* codes, float* latents, float* loss_pf,
                     float* z_q_is, float* z_q, float* mask, float* ws, hipStream_t st) {
   const int F = (frames + FU_NP - 1) / FU_NP;
   size_t lds = (size_t)ChainLds(nq, F, 256 * NM).total * sizeof(float);
-  const size_t lds_pj = (size_t)PJ_CPS * PJ2_LD * sizeof(float);
+  const size_t lds_pj = PJ3 ? (size_t)PJ3_LDS : (size_t)PJ_CPS * PJ2_LD * sizeof(float);
   if (lds < lds_pj) lds = lds_pj;
   if (lds > 80 * 1024) return FUSED_NA;
-  const int cap = fused_clip_capacity<NM>(lds);
+  const int cap = fused_clip_capacity<NM, PJ3>(lds);
   if (cap < 1) return FUSED_NA;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)rvq_fused_kernel<NM>,
+    hipError_t e = hipFuncSetAttribute((const void*)rvq_fused_kernel<NM, PJ3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
@@ -1330,8 +1480,8 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
     f.zsh = zsh;
     f.zsh_bytes = (int)((size_t)bc * nq * FU_NP * FU_ROWS * RCD * sizeof(float));
     f.stamps = g_fstamps;
-    hipLaunchKernelGGL(rvq_fused_kernel<NM>, dim3((unsigned)(2 * bc * FU_NP)), dim3(CH_NT), lds, st,
-                       f);
+    hipLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)), dim3(CH_NT),
+                       lds, st, f);
     const int rc = vrvq_launch_status();
     if (rc) return rc;
   }
@@ -1354,7 +1504,7 @@ extern "C" int vrvq_debug_set_fused_stamps(unsigned long long* buf) {
 
 extern "C" int vrvq_rvq_project_variant(int variant) {
   const int prev = project_variant();
-  if (variant == 1 || variant == 2) g_project_variant = variant;
+  if (variant >= 1 && variant <= 3) g_project_variant = variant;
   else if (variant != 0) return VRVQ_ERR_ARG;
   return prev;
 }
@@ -1496,12 +1646,19 @@ extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, i
     f.w_out = w_out;
     f.b_out = b_out;
     int rc = FUSED_NA;
+    const bool pj3 = project_variant() == 3;
+#define VRVQ_FUSED_CASE(NMV)                                                                    \
+  rc = pj3 ? launch_fused_nm<NMV, true>(f, batch, frames, nq, z, imp, codes, latents, loss_pf,  \
+                                        z_q_is, z_q, mask, part, st)                          \
+           : launch_fused_nm<NMV, false>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, \
+                                         z_q_is, z_q, mask, part, st)
     switch (ncode / 256) {
-      case 1: rc = launch_fused_nm<1>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
-      case 2: rc = launch_fused_nm<2>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
-      case 3: rc = launch_fused_nm<3>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
-      default: rc = launch_fused_nm<4>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask, part, st); break;
+      case 1: VRVQ_FUSED_CASE(1); break;
+      case 2: VRVQ_FUSED_CASE(2); break;
+      case 3: VRVQ_FUSED_CASE(3); break;
+      default: VRVQ_FUSED_CASE(4); break;
     }
+#undef VRVQ_FUSED_CASE
     if (rc != FUSED_NA) return rc;
   }
   int rc = launch_project(z, batch, frames, nq, w_in_t, part, st);
