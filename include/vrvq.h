@@ -62,6 +62,15 @@ int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv, vrvq_stre
 int vrvq_snake(const float* x, int batch, int channels, int frames, const float* alpha,
                const float* inv_alpha, float* y, vrvq_stream_t stream);
 
+/* Phase-split view y[b][c*stride + r][m] = snake_c(x[b][c][m*stride + r - pad]) (alpha NULL: no
+ * Snake; 0 outside [0, frames)), m < out_frames, stride a power of two. Turns a stride-s
+ * product over k = 2s taps (j = q s + r) into a stride-1 2-tap one: the training step's weight
+ * gradients of the strided WNConv1d (models/layers.py:79-85) and WNConvTranspose1d
+ * (:97-103) run on the x3 kernel over it. y may not alias x. */
+int vrvq_phase_split(const float* x, int batch, int channels, int frames, int stride, int pad,
+                     int out_frames, const float* alpha, const float* inv_alpha, float* y,
+                     vrvq_stream_t stream);
+
 /* Codebook normalisation for VectorQuantize.decode_latents (models/quantize.py:92-99):
  * cbn[n,:] = cb[n,:] / max(||cb[n,:]||, 1e-12); c2[n] = sum_k cbn[n,k]^2.
  * cb is [rows][dim] (rows = nq * codebook_size for a stacked RVQ). */
@@ -235,6 +244,14 @@ int vrvq_rvq_path(int path);
  * launch runs on with garbage. *code = that code (1 projection wait, 2 stage wait) or 0, and it
  * is cleared. Synchronises the stream. */
 int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code);
+
+/* Kernel timing of the fused launch (bench.py's roofline): while on (process-wide), every fused
+ * launch of vrvq_rvq_encode carries a pair of HIP events in its own dispatch
+ * (hipExtLaunchKernelGGL), i.e. the kernel's duration on its stream. Returns the previous
+ * setting. vrvq_rvq_timing_read waits for the recorded launches and returns the mean duration
+ * (ms) and their count, then forgets them. */
+int vrvq_rvq_timing(int on);
+int vrvq_rvq_timing_read(float* mean_ms, int* count);
 
 /* The whole quantizer, the replacement of VBRResidualVectorQuantize.forward's quantizer loop,
  * importance mask and masked sum (models/quantize.py:353-365, 389-421) and of

@@ -62,9 +62,10 @@ def test_argument_errors_raise_before_launch():
                                  [0, None])) == 10001
     n = ctypes.c_longlong(0)
     assert lib.vrvq_rvq_workspace(32, 87, 8, ctypes.byref(n)) == 0
-    # partials + the larger of the zst rows (B T nq d) and the fused launch's stage hand-off
-    # rows (B nq 8 parts x 16 frames x d)
-    assert n.value == (8 * 32 * 87 * 64 + max(32 * 87 * 8 * 8, 32 * 8 * 8 * 16 * 8)) * 4
+    # partials as tagged granules (8 B each, the fused launch) + the larger of the zst rows
+    # (B T nq d floats) and the fused launch's tagged stage granules (B nq 8 parts x 16 frames
+    # x d x 8 B)
+    assert n.value == (2 * 8 * 32 * 87 * 64 + max(32 * 87 * 8 * 8, 32 * 8 * 8 * 16 * 8 * 2)) * 4
     assert lib.vrvq_rvq_path(7) == 10001 and lib.vrvq_rvq_path(0) in (1, 2)
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)

@@ -152,8 +152,8 @@ def test_wgrad_deterministic():
 ])
 def test_wgrad_c_abi_in_kernel_snake(m, c, k, stride, pad, dil, T):
     """vrvq_conv1d_wgrad with alpha / alpha_a set (the Snake applied by the kernels while they
-    stage the operands) returns the same bits as the torch op's path (Snake precomputed by
-    vrvq_snake, nullptr alphas): the public C entry point the op no longer takes, per kernel."""
+    stage the operands) returns the same bits as with the operands Snake'd up front by vrvq_snake
+    and nullptr alphas (the form the torch op uses): the public C entry point, per kernel."""
     from vrvq_amd import _lib
     import ctypes
     g0 = torch.Generator().manual_seed(m + c + k)
@@ -164,18 +164,24 @@ def test_wgrad_c_abi_in_kernel_snake(m, c, k, stride, pad, dil, T):
     al_a = (torch.rand(m, generator=g0) + 0.5).to(DEV)
     al_x = (torch.rand(c, generator=g0) + 0.5).to(DEV)
     inv_a, inv_x = ops.snake_inv_alpha(al_a), ops.snake_inv_alpha(al_x)
-    want = ops.conv1d_wgrad(a, x, k, stride, pad, dil, snake_a=(al_a, inv_a),
-                            snake_x=(al_x, inv_x))
+    P = lambda v: ctypes.c_void_p(v.data_ptr()) if v is not None else None  # noqa: E731
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a_s, x_s = torch.empty_like(a), torch.empty_like(x)
+    _lib.call("vrvq_snake", P(a), B, m, ta, P(al_a), P(inv_a), P(a_s), stream)
+    _lib.call("vrvq_snake", P(x), B, c, T, P(al_x), P(inv_x), P(x_s), stream)
     split, ws_bytes = ctypes.c_int(0), ctypes.c_longlong(0)
     _lib.call("vrvq_wgrad_plan", B, m, ta, c, k, ctypes.byref(split), ctypes.byref(ws_bytes))
     ws = torch.empty((ws_bytes.value + 3) // 4, device=DEV)
-    out = torch.empty(m, c, k, device=DEV)
-    P = lambda v: ctypes.c_void_p(v.data_ptr())  # noqa: E731
-    _lib.call("vrvq_conv1d_wgrad", P(a), B, m, ta, P(al_a), P(inv_a), P(x), c, T, P(al_x),
-              P(inv_x), k, stride, pad, dil, split.value, P(ws), ws.numel() * 4, P(out),
-              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+    def wgrad(aa, a_al, a_ia, xx, x_al, x_ia):
+        out = torch.empty(m, c, k, device=DEV)
+        _lib.call("vrvq_conv1d_wgrad", P(aa), B, m, ta, P(a_al), P(a_ia), P(xx), c, T, P(x_al),
+                  P(x_ia), k, stride, pad, dil, split.value, P(ws), ws.numel() * 4, P(out), stream)
+        return out
+    got = wgrad(a, al_a, inv_a, x, al_x, inv_x)
+    want = wgrad(a_s, None, None, x_s, None, None)
     torch.cuda.synchronize()
-    assert torch.equal(out, want)
+    assert torch.equal(got, want)
 
 
 # ------------------------------------------------------------------ mask STE

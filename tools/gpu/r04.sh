@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r04}
-STEPS=${STEPS:-"fused rvqb stamps conv bench knob rvqprof prof"}
+STEPS=${STEPS:-"fused rvqb stamps conv train bench knob rvqprof prof"}
 run() { local name=$1 to=$2; shift 2
   echo "=== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1; local rc=$?
   echo "=== $name rc=$rc"; grep -v amdgpu.ids "gpurun_out/${TAG}_$name.log" | grep -v "^[EW]20" | tail -${TAIL:-5}
@@ -20,7 +20,8 @@ has conv && run conv_tests 400 $PT tests/test_gpu_parity.py -k "conv or strided 
 has bench && run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 has knob && run bench_bn96 300 env VRVQ_CONV_BN96_MIN=200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 has knob && run bench_v2 300 env VRVQ_RVQ_PROJECT=2 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
-has rvqprof && run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_rvq -o run --output-format csv -- python tools/rvq_bench.py --batch 32 --nq 8 --iters 20 --paths 2
+has rvqprof && run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_rvq -o run --output-format csv -- python tools/rvq_bench.py --batch 32 --nq 8 --iters 20 --paths 2 --variants 3
 has prof && run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+has train && run train_tests 400 $PT tests/test_gpu_train.py -k "wgrad or snake_conv_grads or golden"
 has all && run gpu_tests 900 $PT tests -m gpu
 exit 0

@@ -2,8 +2,9 @@
 """Timeline of the fused RVQ launch (rvq_fused_kernel) from in-kernel s_memrealtime stamps
 (100 MHz, one clock for the whole chip; diagnostic build vrvq_amd/libvrvq_hip_stamps.so, built
 with `python -m vrvq_amd.build --stamps`). Thread 0 of every workgroup records:
-  projection / chain workgroups: 0 start | 1 partials stored + drained | 2 the clip's 8 units
-      seen | 3 chain prologue done | 4 + i end of stage i | 36 epilogue done
+  projection / chain workgroups: 0 start | 44 z slab in LDS (x3 projection) | 45 projection
+      MFMAs done, partial granules issued | 2 thread 0's partials seen (tags valid) | 3 chain
+      prologue done | 4 + i end of stage i | 36 epilogue done
   expansion workgroups: 0 start | 1 + i stage i starts (its wait passed) | 40 all stages done |
       41 z_q stored
 Prints, in us from the first workgroup's start, the median and max over workgroups."""
@@ -83,8 +84,9 @@ def main():
     print(f"B={B} nq={nq} T={T}: {B * 8} projection/chain + {B * 8} expansion workgroups (us)")
     print("projection / chain workgroups")
     row("start", pc[:, 0])
-    row("partials stored", pc[:, 1])
-    row("clip's projection seen", pc[:, 2])
+    row("z slab in LDS", pc[:, 44])
+    row("projection MFMAs + stores issued", pc[:, 45])
+    row("clip's partials seen (thread 0)", pc[:, 2])
     row("prologue done", pc[:, 3])
     for i in range(nq):
         row(f"stage {i} end", pc[:, 4 + i])

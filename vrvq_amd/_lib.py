@@ -22,6 +22,7 @@ SIGNATURES = {
     "vrvq_weight_norm": [_P, _P, _I, _I, _P, _P],
     "vrvq_snake_inv_alpha": [_P, _I, _P, _P],
     "vrvq_snake": [_P, _I, _I, _I, _P, _P, _P, _P],
+    "vrvq_phase_split": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
@@ -74,7 +75,8 @@ SIGNATURES = {
 }
 EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
          "vrvq_rvq_project_variant": ([_I], _I), "vrvq_rvq_path": ([_I], _I),
-         "vrvq_rvq_sync_error": ([_P, _P], _I)}
+         "vrvq_rvq_sync_error": ([_P, _P], _I), "vrvq_rvq_timing": ([_I], _I),
+         "vrvq_rvq_timing_read": ([_P, _P], _I)}
 
 _lock = threading.Lock()
 _lib = None
@@ -128,6 +130,19 @@ def rvq_sync_error(stream: int) -> int:
     code = ctypes.c_int(0)
     call("vrvq_rvq_sync_error", ctypes.c_void_p(stream), ctypes.byref(code))
     return code.value
+
+
+def rvq_timing(on: bool) -> bool:
+    """Attach HIP start / stop events to every fused RVQ launch (kernel duration on its stream)
+    while on. Returns the previous setting."""
+    return bool(load().vrvq_rvq_timing(1 if on else 0))
+
+
+def rvq_timing_read():
+    """(mean kernel ms, launches) of the launches recorded since the last read."""
+    ms, n = ctypes.c_float(0.0), ctypes.c_int(0)
+    call("vrvq_rvq_timing_read", ctypes.byref(ms), ctypes.byref(n))
+    return float(ms.value), int(n.value)
 
 
 def rvq_project_variant(variant: int = 0) -> int:

@@ -51,10 +51,15 @@ constexpr int x3_stages() { return BM * BN <= 128 * 128 ? 1 : 2; }
 // K-chunk) measured slower: profiles/r03_x3_pair_ab.txt.
 // The same pairing for the 2-tap GEMMs (the strided encoder convs through the phase-split view
 // and the polyphase ConvTranspose): 32-channel K-chunks of 8 octets = 4 MFMA steps (the
-// 16-channel chunk has 2), on tiles up to 128 x 128 (one LDS stage, two workgroups per CU).
+// 16-channel chunk has 2), on the 128- and 32-wide tiles up to 128 rows (one LDS stage, two
+// workgroups per CU). Measured per layer at B = 32 (profiles/r04d_layer_table.txt vs
+// r03f_layer_table.txt): 128 x 128 tiles 5-13 % faster (64->128 s2, 128->256 s4, ConvT 384->192
+// s4), 128 x 32 10 % (512->1024 s8 at T = 87); 128 x 64 and 128 x 96 4-14 % slower (the doubled
+// weight stage costs the 128 x 64 tile its third workgroup per CU): those keep 16-channel chunks.
 template <int KS, int BM, int BN>
 constexpr bool x3_pair() {
-  return (KS == 7 && BM == 64 && BN == 256) || (KS == 2 && BM <= 128 && BN <= 128);
+  return (KS == 7 && BM == 64 && BN == 256) ||
+         (KS == 2 && BM <= 128 && (BN == 128 || BN == 32));
 }
 
 template <int KS, bool PAIR = false>

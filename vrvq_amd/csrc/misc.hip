@@ -293,6 +293,49 @@ extern "C" int vrvq_snake(const float* x, int batch, int channels, int frames, c
   return vrvq_launch_status();
 }
 
+// Phase-split view of a (Snake-activated) signal: y[b][c s + r][m] = snake_c(x[b][c][m s + r -
+// pad]), 0 outside [0, frames). A stride-s product over taps j = q s + r (q = 0, 1) becomes a
+// stride-1 2-tap one over the view (the forward x3 path addresses the same view while staging;
+// the weight gradients of the strided encoder convs and of the ConvTranspose layers take it
+// materialised, once per layer). Thread = one view element; the gathers read rows of x.
+__global__ __launch_bounds__(256) void phase_split_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ alpha,
+                                                          const float* __restrict__ inv_alpha,
+                                                          int channels, int frames, int sh,
+                                                          int pad, int out_frames,
+                                                          float* __restrict__ y, long long n) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;  // no barrier in this kernel
+  const int m = (int)(e % out_frames);
+  const long long rowv = e / out_frames;                 // b * (channels << sh) + c s + r
+  const int vr = (int)(rowv % ((long long)channels << sh));
+  const long long b = rowv / ((long long)channels << sh);
+  const int c = vr >> sh, r = vr & ((1 << sh) - 1);
+  const int t = (m << sh) + r - pad;
+  float v = 0.0f;
+  if (t >= 0 && t < frames) {
+    v = x[(b * channels + c) * (long long)frames + t];
+    if (alpha) v = snake_act(v, alpha[c], inv_alpha[c]);
+  }
+  y[e] = v;
+}
+
+extern "C" int vrvq_phase_split(const float* x, int batch, int channels, int frames, int stride,
+                                int pad, int out_frames, const float* alpha,
+                                const float* inv_alpha, float* y, vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && y && x != y && batch > 0 && channels > 0 && frames > 0 && out_frames > 0);
+  VRVQ_CHECK_ARG(stride > 0 && (stride & (stride - 1)) == 0 && pad >= 0);
+  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
+  int sh = 0;
+  while ((1 << sh) < stride) ++sh;
+  const long long n = (long long)batch * channels * stride * out_frames;
+  const long long nblk = (n + 255) / 256;
+  if (nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
+  hipLaunchKernelGGL(phase_split_kernel, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), x,
+                     alpha, inv_alpha, channels, frames, sh, pad, out_frames, y, n);
+  return vrvq_launch_status();
+}
+
 extern "C" int vrvq_snake_inv_alpha(const float* alpha, int channels, float* inv,
                                     vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(alpha && inv && channels > 0);

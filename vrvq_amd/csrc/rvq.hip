@@ -25,11 +25,27 @@
 //
 // Codes of every golden fixture are reproduced bit for bit (the same fp32 expression for the
 // distance as the reference: dot in k order, fma(d, -2, e2) + c2, lowest index on ties).
+#include <hip/hip_ext.h>
+
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 #include "lanes.h"
+
+#ifdef VRVQ_STAMPS
+// Fused launch (rvq_fused_kernel), diagnostic build: thread 0 of every workgroup records
+// s_memrealtime (100 MHz, one clock for the whole chip) at its phase boundaries into
+// stamps[blockIdx][64] (tools/rvq_fused_stamps.py).
+#define FSTAMP(buf, slot)                                                                    \
+  do {                                                                                     \
+    if ((buf) && threadIdx.x == 0)                                                         \
+      (buf)[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+#else
+#define FSTAMP(buf, slot) do {} while (0)
+#endif
 
 namespace {
 
@@ -50,6 +66,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr int CPOL_SC1 = 16;    // buffer load / store aux: sc1 (L1 bypass, write-through)
 constexpr int RSRC_FLAGS = 0x00020000;  // raw buffer descriptor word 3 (gfx950)
 
@@ -245,17 +262,20 @@ constexpr int PJ2_LD = 112;                     // z_s row stride (112 = 48 mod 
 constexpr int PJ2_ZQ = PJ_KC * PJ2_TC / PJ2_NT; // z loads per thread per K chunk (6)
 
 // Where the partials go: plain stores (the three-launch path: the chain reads them after a
-// kernel boundary) or write-through sc1 16-B stores (the fused launch: read by other workgroups
-// of the same launch with sc1 loads, MI355X_MICROARCH.md visibility table, first row).
+// kernel boundary) or, in the fused launch, tagged 8-B granules {partial, tag} written
+// through (sc1, 16-B stores = two whole granules): the data is its own flag, the consumer
+// checks the tags of what it read (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16,
+// R2) -- no drain, no flag word.
 struct PartSink {
   float* part;
-  __amdgpu_buffer_rsrc_t rsrc;
-  bool sc1;
+  __amdgpu_buffer_rsrc_t rsrc;  // over the granule buffer (tag != 0)
+  unsigned tag;                 // 0: plain floats
   __device__ __forceinline__ void put(size_t off, float4 v) const {
-    if (sc1) {
-      u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                 __float_as_uint(v.w)};
-      __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, (int)(off * 4), 0, CPOL_SC1);
+    if (tag) {
+      const u32x4 g0 = {__float_as_uint(v.x), tag, __float_as_uint(v.y), tag};
+      const u32x4 g1 = {__float_as_uint(v.z), tag, __float_as_uint(v.w), tag};
+      __builtin_amdgcn_raw_buffer_store_b128(g0, rsrc, (int)(off * 8), 0, CPOL_SC1);
+      __builtin_amdgcn_raw_buffer_store_b128(g1, rsrc, (int)(off * 8 + 16), 0, CPOL_SC1);
     } else {
       *reinterpret_cast<float4*>(part + off) = v;
     }
@@ -353,7 +373,7 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project2_kernel(const float* __res
                                                               const float* __restrict__ w_in_t,
                                                               float* __restrict__ part, int NF) {
   __shared__ __attribute__((aligned(16))) float z_s[PJ_CPS * PJ2_LD];
-  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), false};
+  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), 0u};
   project2_body(z, T, nq, blockIdx.x % n_tc, blockIdx.x / n_tc, blockIdx.y, w_in_t, out, NF, z_s);
 }
 
@@ -394,13 +414,32 @@ __device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
 
 __device__ __forceinline__ void project3_body(const float* __restrict__ z, int T, int nq, int tc,
                                               int b, int s, const float* __restrict__ w_in_t,
-                                              const PartSink& out, int NF, char* lds) {
+                                              const PartSink& out, int NF, char* lds,
+                                              unsigned long long* stamps = nullptr) {
   constexpr int NIT = (PJ_CPS / 8) * PJ2_TC / PJ2_NT;  // (octet, frame) items per thread: 3
+  constexpr int NKS = PJ_CPS / 32;                      // K steps of 32 channels
   const int R = nq * RCD;
   const int t0 = tc * PJ2_TC;
   const int ntl = min(PJ2_TC, T - t0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_rt = (R + 15) / 16;
+  const int lr = lane & 15, kg = lane >> 4;
+  // A operands of a work item (16-row tile rt): row r = 16 rt + lr, channels 32 ks + 8 kg .. +7
+  // of the split (w_in_t[stage][c][k]); rows >= R zeroed
+  auto load_w = [&](int rt, float (&w)[NKS][8]) {
+    const int r = rt * 16 + lr;
+    const unsigned rm = 0u - (unsigned)(r < R);
+    const float* wp = w_in_t + ((size_t)min(r >> 3, nq - 1) * RD + s * PJ_CPS + 8 * kg) * RCD + (r & 7);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        w[ks][u] = __uint_as_float(__float_as_uint(wp[(size_t)(32 * ks + u) * RCD]) & rm);
+  };
+  float w[NKS][8];
+  // the first item's weights (L2) first: their latency runs under the z slab's
+  load_w(min(wave, 2 * n_rt - 1) >> 1, w);
   const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
   {  // the slab: every load in flight, then split and stored transposed
     float zv[NIT][8];
@@ -428,34 +467,28 @@ __device__ __forceinline__ void project3_body(const float* __restrict__ z, int T
       *reinterpret_cast<u32x4*>(d + 2 * PJ3_PLANE) = u32x4{l[0], l[1], l[2], l[3]};
     }
   }
+  // a use of the weights here keeps their loads ahead of the slab's (else they are sunk below
+  // the barrier and waited for one K step at a time)
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) asm volatile("" ::"v"(w[ks][u]));
   __syncthreads();
+  FSTAMP(stamps, 44);
   // work items (16-row tile rt, half hf = frame tiles 3 hf .. 3 hf + 2) over the 8 waves
-  const int n_rt = (R + 15) / 16;
-  const int lr = lane & 15, kg = lane >> 4;
   for (int item = wave; item < 2 * n_rt; item += PJ2_NT / 64) {
     const int rt = item >> 1, hf = item & 1;
-    // A: row r = 16 rt + lr, channels 32 ks + 8 kg .. +7 of the split (w_in_t[stage][c][k])
-    const int r = rt * 16 + lr;
-    const unsigned rm = 0u - (unsigned)(r < R);
-    const float* wp = w_in_t + ((size_t)min(r >> 3, nq - 1) * RD + s * PJ_CPS + 8 * kg) * RCD + (r & 7);
-    float wn[8];  // the next K step's 8 weights in flight while this step's MFMAs run
-#pragma unroll
-    for (int u = 0; u < 8; ++u) wn[u] = __uint_as_float(__float_as_uint(wp[(size_t)u * RCD]) & rm);
+    if (item != wave) load_w(rt, w);
     f32x4 acc[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < PJ_CPS / 32; ++ks) {
+    for (int ks = 0; ks < NKS; ++ks) {
       unsigned h[4], mm[4], l[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) rvq_split3x2(wn[2 * u], wn[2 * u + 1], h[u], mm[u], l[u]);
+      for (int u = 0; u < 4; ++u) rvq_split3x2(w[ks][2 * u], w[ks][2 * u + 1], h[u], mm[u], l[u]);
       const u32x4 ah = {h[0], h[1], h[2], h[3]}, am = {mm[0], mm[1], mm[2], mm[3]},
                   al = {l[0], l[1], l[2], l[3]};
-      if (ks + 1 < PJ_CPS / 32) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          wn[u] = __uint_as_float(__float_as_uint(wp[(size_t)(32 * (ks + 1) + u) * RCD]) & rm);
-      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const char* bp = lds + ((3 * hf + j) * 16 + lr) * (PJ3_LDB * 2) + (32 * ks + 8 * kg) * 2;
@@ -492,7 +525,7 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project3_kernel(const float* __res
                                                               const float* __restrict__ w_in_t,
                                                               float* __restrict__ part, int NF) {
   extern __shared__ __attribute__((aligned(16))) char lds3[];
-  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), false};
+  PartSink out{part, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0, RSRC_FLAGS), 0u};
   project3_body(z, T, nq, blockIdx.x % n_tc, blockIdx.x / n_tc, blockIdx.y, w_in_t, out, NF, lds3);
 }
 
@@ -545,17 +578,8 @@ struct ChainArgs {
                (step)] = t_;                                                               \
     }                                                                                      \
   } while (0)
-// Fused launch (rvq_fused_kernel): thread 0 of every workgroup records s_memrealtime (100 MHz,
-// one clock for the whole chip) at its phase boundaries into stamps[blockIdx][64]
-// (tools/rvq_fused_stamps.py).
-#define FSTAMP(buf, slot)                                                                    \
-  do {                                                                                     \
-    if ((buf) && threadIdx.x == 0)                                                         \
-      (buf)[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
-  } while (0)
 #else
 #define CSTAMP(stage, step) do {} while (0)
-#define FSTAMP(buf, slot) do {} while (0)
 #endif
 
 // LDS carve (floats), shared by the launcher's size computation.
@@ -618,14 +642,11 @@ __device__ __forceinline__ unsigned wave_wait_ge(const unsigned* flags, int n, u
 }
 
 struct ChainHandoff {              // fused launch only
-  const unsigned* flagp;           // the clip's projection-unit words (PJ_SPLIT)
-  unsigned* flagc;                 // this chain part's publish word
   unsigned* err;
   unsigned epoch;
-  __amdgpu_buffer_rsrc_t part;     // the partials, read with sc1 loads
-  __amdgpu_buffer_rsrc_t zsh;      // the stage hand-off rows, stored sc1
-  int zsh0;                        // float offset of (clip, stage 0, this part)
-  int zsh_stage;                   // floats per stage
+  __amdgpu_buffer_rsrc_t part;     // the partials' tagged granules, read with sc1 loads
+  unsigned long long* zsh;         // this part's stage-0 block of tagged zst granules
+  int zsh_stage;                   // granules per stage
   unsigned long long* stamps;      // diagnostic build only
 };
 
@@ -659,24 +680,57 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
   const int cw = wave * NPW;
   CSTAMP(nq, 0);
 
+  // stage 0's operands first: they do not depend on the projection (fused: the loads run
+  // under the wait for the clip's projection units)
+  for (int e = tid; e < CH_FMAX * RCD; e += CH_NT) e_s[e] = 0.0f;
+  for (int e = tid; e < CH_FMAX; e += CH_NT) e2_s[e] = 0.0f;
+  float av[NT][2];  // cbn fragments of the current stage: code cw + 16 t + fl, k = 4 kh + lg
+  auto load_a = [&](int i, float (&dst)[NT][2]) {  // NT / 2 contiguous float4 per lane
+    const float* src = a.cbf + (((size_t)i * CH_NW + wave) * 64 + lane) * (2 * NT);
+#pragma unroll
+    for (int q = 0; q < NT / 2; ++q) {
+      const float4 v = ld4(src + 4 * q);
+      dst[2 * q][0] = v.x; dst[2 * q][1] = v.y; dst[2 * q + 1][0] = v.z; dst[2 * q + 1][1] = v.w;
+    }
+  };
+  load_a(0, av);
+  for (int e = tid; e < N; e += CH_NT) c2_s[e] = a.c2[e];
+  if (nq > 1)
+    for (int e = tid; e < R * RCD / 4; e += CH_NT)
+      reinterpret_cast<float4*>(m_s)[e] = ld4(a.mcol + (size_t)e * 4);
   // ---- prologue: pu = (P + b_in) - Qb (partials summed in split order); stage 0 operands.
   if constexpr (FUSED) {
-    // wait for the clip's PJ_SPLIT projection units, then read the partials write-through
-    // (sc1) as float4: nf * R / 4 per split (R = 8 nq, the frames' rows are contiguous)
-    if (wave == 0) wave_wait_ge(hx.flagp, PJ_SPLIT, hx.epoch, hx.err, 1u);
-    __syncthreads();
-    FSTAMP(hx.stamps, 2);
+    // the clip's 8 partials of this part's frames: tagged granules (16-B sc1 loads, two each),
+    // each thread re-reads its item until every tag is this call's (the projection units of
+    // the clip run concurrently on other CUs); R = 8 nq: the frames' rows are contiguous
+    const unsigned ptag = hx.epoch * 64u;
     for (int e4 = tid; e4 < nf * R / 4; e4 += CH_NT) {
-      u32x4 v[PJ_SPLIT];
+      u32x4 v[PJ_SPLIT][2];
+      for (unsigned it = 0;; ++it) {
 #pragma unroll
-      for (int sp = 0; sp < PJ_SPLIT; ++sp)
-        v[sp] = __builtin_amdgcn_raw_buffer_load_b128(
-            hx.part, (int)((((size_t)sp * a.NF + n0) * R + 4 * e4) * 4), 0, CPOL_SC1);
+        for (int sp = 0; sp < PJ_SPLIT; ++sp) {
+          const int off = (int)((((size_t)sp * a.NF + n0) * R + 4 * e4) * 8);
+          v[sp][0] = __builtin_amdgcn_raw_buffer_load_b128(hx.part, off, 0, CPOL_SC1);
+          v[sp][1] = __builtin_amdgcn_raw_buffer_load_b128(hx.part, off + 16, 0, CPOL_SC1);
+        }
+        bool ok = true;
+#pragma unroll
+        for (int sp = 0; sp < PJ_SPLIT; ++sp)
+          ok = ok && v[sp][0][1] == ptag && v[sp][0][3] == ptag && v[sp][1][1] == ptag &&
+               v[sp][1][3] == ptag;
+        if (ok) break;
+        if (it == SPIN_MAX) {
+          st_flag(hx.err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      FSTAMP(hx.stamps, 2);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float pv = __uint_as_float(v[0][j]);
+        float pv = __uint_as_float(v[0][j >> 1][2 * (j & 1)]);
 #pragma unroll
-        for (int sp = 1; sp < PJ_SPLIT; ++sp) pv = pv + __uint_as_float(v[sp][j]);
+        for (int sp = 1; sp < PJ_SPLIT; ++sp) pv = pv + __uint_as_float(v[sp][j >> 1][2 * (j & 1)]);
         const int e = 4 * e4 + j, r = e % R;
         pu_s[e] = (pv + a.b_in[r]) - a.qb[r];
       }
@@ -704,22 +758,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
       }
     }
   }
-  for (int e = tid; e < CH_FMAX * RCD; e += CH_NT) e_s[e] = 0.0f;
-  for (int e = tid; e < CH_FMAX; e += CH_NT) e2_s[e] = 0.0f;
-  float av[NT][2];  // cbn fragments of the current stage: code cw + 16 t + fl, k = 4 kh + lg
-  auto load_a = [&](int i, float (&dst)[NT][2]) {  // NT / 2 contiguous float4 per lane
-    const float* src = a.cbf + (((size_t)i * CH_NW + wave) * 64 + lane) * (2 * NT);
-#pragma unroll
-    for (int q = 0; q < NT / 2; ++q) {
-      const float4 v = ld4(src + 4 * q);
-      dst[2 * q][0] = v.x; dst[2 * q][1] = v.y; dst[2 * q + 1][0] = v.z; dst[2 * q + 1][1] = v.w;
-    }
-  };
-  load_a(0, av);
-  for (int e = tid; e < N; e += CH_NT) c2_s[e] = a.c2[e];
-  if (nq > 1)
-    for (int e = tid; e < R * RCD / 4; e += CH_NT)
-      reinterpret_cast<float4*>(m_s)[e] = ld4(a.mcol + (size_t)e * 4);
   __syncthreads();
   float ze = 0.0f;  // S2 lanes: z_e of (rf, rk) at the current stage
   auto set_e = [&](float zv) {  // F.normalize (eps 1e-12) of the 8-lane group's z_e
@@ -864,15 +902,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     CSTAMP(i, 3);
     __syncthreads();  // ------------------------------- candidates, stage i+1's c2 / M ready
     CSTAMP(i, 4);
-    if constexpr (FUSED) {
-      // the S2 waves publish stage i-1: its zst rows were stored write-through in S2 of stage
-      // i-1 (a stage ago, so this drain waits for nothing but this stage's prefetch, which the
-      // end of S2 needs anyway); each wave signals for its own stores
-      if (wave < 2 && i > 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) st_flag(hx.flagc + wave, hx.epoch * 64u + (unsigned)i);
-      }
-    }
     // ---- S2 (role lanes) ----
     int bi = 0;
     float zq = 0.0f;
@@ -897,11 +926,18 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     }
     const float zsv = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
     if constexpr (FUSED) {
-      // waves 0-1 = frames 0..15 x k: the part's 16-frame row block of this stage, two whole
-      // 256-B runs (frames >= nf store 0), one sc1 store per wave
-      if (wave < 2)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsv), hx.zsh,
-                                              (hx.zsh0 + i * hx.zsh_stage + tid) * 4, 0, CPOL_SC1);
+      // waves 0-1 = frames 0..15 x k: the part's 16-frame block of this stage as tagged 8-B
+      // granules {zst, 64 epoch + i + 1} (one sc1 store each: the data is its own flag, no
+      // drain, no flag word), k = 2 s + h at slot 4 h + s of the frame (a consumer lane's four
+      // k values are 32 contiguous bytes); frames >= nf store 0 with the tag
+      if (wave < 2) {
+        const unsigned long long g =
+            ((unsigned long long)(hx.epoch * 64u + (unsigned)i + 1u) << 32) |
+            __float_as_uint(zsv);
+        __hip_atomic_store((gu64*)(hx.zsh + (size_t)i * hx.zsh_stage + (rf * 8 + (rk & 1) * 4 +
+                                                                          (rk >> 1))),
+                           g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     const float diff = ze - zq;
     const float l2 = vrvq::sum8(diff * diff, lane);
@@ -937,12 +973,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     if constexpr (FUSED) FSTAMP(hx.stamps, 4 + i);
   }
   CSTAMP(nq, 2);
-  if constexpr (FUSED) {  // publish the last stage
-    if (wave < 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) st_flag(hx.flagc + wave, hx.epoch * 64u + (unsigned)nq);
-    }
-  }
 
   // ---- epilogue: outputs of every stage (LDS -> HBM)
   for (int e = tid; e < nf * nq * RCD; e += CH_NT) {
@@ -1082,8 +1112,6 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 constexpr int FU_NP = PJ_SPLIT;     // chain parts per clip
 constexpr int FU_ROWS = 16;         // frames per part block of the stage hand-off rows
 constexpr int FU_CB = 128;          // channels per expansion workgroup
-constexpr int SYNC_FLAGP = 0;       // sync block words: [clip * 32 + split]
-constexpr int SYNC_FLAGC = 1024;    //                   [clip * 32 + 2 part + wave]
 constexpr int SYNC_ERR = 2048;      //                   first timeout code (1 projection, 2 stage)
 constexpr int SYNC_WORDS = 2052;    // used words (x 4 = 8208 B, a multiple of 16)
 constexpr int FU_CLIPS_MAX = 32;    // clips per launch (flag slots)
@@ -1096,7 +1124,7 @@ struct FusedArgs {
   const float* b_out;               // [nq][D]
   float* z_q_is;                    // [B][nq][D][T] or null
   float* z_q;                       // [B][D][T]
-  float* zsh;                       // [B][nq][FU_NP][FU_ROWS][8] stage hand-off rows
+  unsigned long long* zsh;          // [B][nq][FU_NP][FU_ROWS][8] tagged zst granules
   int zsh_bytes;
   unsigned* sync;
   unsigned epoch;
@@ -1105,9 +1133,20 @@ struct FusedArgs {
 
 // Expansion workgroup (clip b, channels [128 cb, +128)): wave w = 32-channel tile (w & 3) x
 // 32-frame tiles {w >> 2, (w >> 2) + 2}; per stage five v_mfma_f32_32x32x2_f32 per tile exactly
-// as rvq_expand_kernel (K = 10: W_out x zst, bias x 1). It waits for the stages in batches: every
-// stage the clip's parts have all published when it looks, then the next wait.
-__device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, float* sm) {
+// as rvq_expand_kernel (K = 10: W_out x zst, bias x 1). Every wave runs on its own (no barrier).
+// The stage's zst rows are tagged granules (the chain's S2 stores): a wave loads stage i + 1's
+// granules (and W_out / b_out rows) speculatively BEFORE stage i's z_q_is stores and checks
+// their tags when it gets there -- vmcnt retires in order, so a load issued after the stores
+// would wait for them to drain (with flag words trailing the data the workgroup ran ~4 us per
+// stage, bound by its own store queue: profiles/r04d_fused_timeline.txt). Rows whose tags are
+// not this call's stage yet are re-read until they are (bounded).
+struct ExOps {
+  float4 w0, w1;
+  float bb;
+  u32x4 z[2][2];  // per frame tile: 4 granules {zst k = 2 s + h, tag}, s = 0..3
+};
+
+__device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
   const int nq = f.c.nq, T = f.c.T, F = f.c.F;
   const int b = e / (RD / FU_CB), cb = e - b * (RD / FU_CB);
   const int lane = threadIdx.x & 63;
@@ -1119,7 +1158,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   const bool two = ft0 + 2 < n_ft;  // wave-uniform
   const __amdgpu_buffer_rsrc_t zr =
       __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
-  int zoff[2];
+  int zoff[2];  // byte offset of this lane's 4 granules of stage 0
   int tt[2];
   bool tv[2];
   float sc[2];
@@ -1130,62 +1169,100 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
     tv[j] = t < T && (j == 0 || two);
     const int tc = min(t, T - 1);
     const int p = tc / F, fr = tc - p * F;
-    zoff[j] = ((b * nq * FU_NP + p) * FU_ROWS + fr) * RCD;  // stage 0
+    zoff[j] = (((b * nq * FU_NP + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
     sc[j] = (f.c.imp && tv[j]) ? (f.c.imp[(size_t)b * T + tc] * f.c.level) * (float)nq : INFINITY;
   }
-  const int zstage = FU_NP * FU_ROWS * RCD;
+  const int zstage = FU_NP * FU_ROWS * RCD * 8;  // bytes per stage
   const int cr = c0 + col;  // A-operand row of this lane
   const float* wp = f.w_out + (size_t)cr * RCD;
   const size_t wstride = (size_t)RD * RCD;
+  const unsigned base = f.epoch * 64u;
+  auto load_z = [&](int i, u32x4 (&z)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int off = zoff[j] + i * zstage;
+      z[j][0] = __builtin_amdgcn_raw_buffer_load_b128(zr, off, 0, CPOL_SC1);
+      z[j][1] = __builtin_amdgcn_raw_buffer_load_b128(zr, off + 16, 0, CPOL_SC1);
+    }
+  };
+  auto load = [&](int i, ExOps& o) {
+    o.w0 = ld4(wp + i * wstride);
+    o.w1 = ld4(wp + i * wstride + 4);
+    o.bb = f.b_out[(size_t)i * RD + cr];
+    load_z(i, o.z);
+  };
+  auto tagged = [&](const u32x4 (&z)[2][2], int i) -> bool {  // wave-uniform
+    const unsigned tag = base + (unsigned)i + 1u;
+    bool good = true;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (j == 0 || two)
+        good = good && z[j][0][1] == tag && z[j][0][3] == tag && z[j][1][1] == tag &&
+               z[j][1][3] == tag;
+    return __builtin_amdgcn_ballot_w64(!good) == 0;
+  };
   f32x16 zq[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) zq[j][r] = 0.0f;
-  unsigned* avail_s = reinterpret_cast<unsigned*>(sm);  // [2]: alternating broadcast words
-  const unsigned base = f.epoch * 64u;
-  bool dead = false;
-  int i = 0;
-  for (int it = 0; i < nq; ++it) {
-    if (wave == 0) {
-      unsigned v = dead ? 0u
-                        : wave_wait_ge(f.sync + SYNC_FLAGC + b * 32, 2 * FU_NP, base + i + 1,
-                                       f.sync + SYNC_ERR, 2u);
-      if (lane == 0) avail_s[it & 1] = v ? v - base : (unsigned)nq;  // timeout: run on
-    }
-    __syncthreads();
-    const int upto = min((int)avail_s[it & 1], nq);
-    dead = dead || upto <= i;  // a wait ran out: no more waits
-    for (; i < upto; ++i) {
-      FSTAMP(f.stamps, 1 + i);
-      const float4 w0 = ld4(wp + i * wstride), w1 = ld4(wp + i * wstride + 4);
-      const float bb = f.b_out[(size_t)i * RD + cr];
-      const float wa[4] = {h ? w0.y : w0.x, h ? w0.w : w0.z, h ? w1.y : w1.x, h ? w1.w : w1.z};
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (j == 1 && !two) break;
-        const int off = (zoff[j] + i * zstage) * 4;
-        const u32x4 z0 = __builtin_amdgcn_raw_buffer_load_b128(zr, off, 0, CPOL_SC1);
-        const u32x4 z1 = __builtin_amdgcn_raw_buffer_load_b128(zr, off + 16, 0, CPOL_SC1);
-        const float zb[4] = {__uint_as_float(h ? z0[1] : z0[0]), __uint_as_float(h ? z0[3] : z0[2]),
-                             __uint_as_float(h ? z1[1] : z1[0]), __uint_as_float(h ? z1[3] : z1[2])};
-        f32x16 q;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) q[r] = 0.0f;
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-          q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
-        q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : bb, h ? 0.0f : 1.0f, q, 0, 0, 0);
-        const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
-        if (f.z_q_is && tv[j]) {
-          float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = q[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) zq[j][r] = zq[j][r] + q[r] * m;
+  ExOps cur;
+  bool dead = false;  // a wait ran out: no more waits (err recorded)
+  // stage 0 lands after the projection and the chain's first stage (~10 us): wave 0 alone
+  // watches its rows with a long sleep between looks, the others wait at the barrier
+  if (wave == 0) {
+    for (unsigned it = 0;; ++it) {
+      load_z(0, cur.z);
+      if (tagged(cur.z, 0)) break;
+      if (it == SPIN_MAX) {
+        if (lane == 0) st_flag(f.sync + SYNC_ERR, 2u);
+        dead = true;
+        break;
       }
+      __builtin_amdgcn_s_sleep(16);
     }
+  }
+  __syncthreads();
+  load(0, cur);
+  for (int i = 0; i < nq; ++i) {
+    for (unsigned it = 0; !dead && !tagged(cur.z, i); ++it) {
+      if (it == SPIN_MAX) {
+        if (lane == 0) st_flag(f.sync + SYNC_ERR, 2u);
+        dead = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+      load_z(i, cur.z);
+    }
+    FSTAMP(f.stamps, 1 + i);
+    // the next stage's operands ahead of this stage's stores (unconditional, clamped stage: a
+    // branch around loads makes the waitcnt pass drain at the join)
+    ExOps nxt;
+    load(min(i + 1, nq - 1), nxt);
+    const float wa[4] = {h ? cur.w0.y : cur.w0.x, h ? cur.w0.w : cur.w0.z,
+                         h ? cur.w1.y : cur.w1.x, h ? cur.w1.w : cur.w1.z};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
+      const float zb[4] = {__uint_as_float(cur.z[j][0][0]), __uint_as_float(cur.z[j][0][2]),
+                           __uint_as_float(cur.z[j][1][0]), __uint_as_float(cur.z[j][1][2])};
+      f32x16 q;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) q[r] = 0.0f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cur.bb, h ? 0.0f : 1.0f, q, 0, 0, 0);
+      const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
+      if (f.z_q_is && tv[j]) {
+        float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = q[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zq[j][r] = zq[j][r] + q[r] * m;
+    }
+    cur = nxt;
   }
   FSTAMP(f.stamps, 40);
 #pragma unroll
@@ -1205,38 +1282,31 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   const int blk = blockIdx.x;
   FSTAMP(f.stamps, 0);
   if (blk >= B * FU_NP) {
-    fused_expand_body(f, blk - B * FU_NP, sm);
+    fused_expand_body(f, blk - B * FU_NP);
     FSTAMP(f.stamps, 41);
     return;
   }
   const int b = blk / FU_NP, s = blk - b * FU_NP;
   const int R = nq * RCD;
-  float* part = const_cast<float*>(f.c.part);  // the workspace this launch writes
+  float* part = const_cast<float*>(f.c.part);  // the workspace this launch writes (granules)
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
-      part, (short)0, (int)((size_t)PJ_SPLIT * f.c.NF * R * 4), RSRC_FLAGS);
-  // projection unit (b, s): partials write-through, every storing wave drained, one flag
-  PartSink out{part, pr, true};
-  if constexpr (PJ3) project3_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, reinterpret_cast<char*>(sm));
+      part, (short)0, (int)((size_t)PJ_SPLIT * f.c.NF * R * 8), RSRC_FLAGS);
+  // projection unit (b, s): partials as tagged granules, then straight on to the chain
+  PartSink out{part, pr, f.epoch * 64u};
+  if constexpr (PJ3)
+    project3_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, reinterpret_cast<char*>(sm),
+                  f.stamps);
   else project2_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, sm);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  FSTAMP(f.stamps, 1);
-  if (threadIdx.x == 0) st_flag(f.sync + SYNC_FLAGP + b * 32 + s, f.epoch);
+  FSTAMP(f.stamps, 45);
+  __syncthreads();  // the slab's LDS is the chain's from here
   // chain part s of clip b
   const int nf = min(F, T - s * F);
-  unsigned* flagc = f.sync + SYNC_FLAGC + b * 32 + 2 * s;
-  if (nf <= 0) {  // no frames (T < 8 F): nothing to publish but the count
-    if (threadIdx.x < 2) st_flag(flagc + threadIdx.x, f.epoch * 64u + (unsigned)nq);
-    return;
-  }
+  if (nf <= 0) return;  // no frames (T < 8 F): no expansion lane reads this part's block
   ChainHandoff hx;
-  hx.flagp = f.sync + SYNC_FLAGP + b * 32;
-  hx.flagc = flagc;
   hx.err = f.sync + SYNC_ERR;
   hx.epoch = f.epoch;
   hx.part = pr;
-  hx.zsh = __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
-  hx.zsh0 = (b * nq * FU_NP + s) * FU_ROWS * RCD;
+  hx.zsh = f.zsh + (size_t)(b * nq * FU_NP + s) * FU_ROWS * RCD;
   hx.zsh_stage = FU_NP * FU_ROWS * RCD;
   hx.stamps = f.stamps;
   chain_body<NM, true>(f.c, sm, b * T + s * F, nf, hx);
@@ -1346,11 +1416,11 @@ bool rvq_shape_ok(int dim, int cdim, int nq, int ncode) {
 
 size_t part_floats(long long nf, int nq) { return (size_t)PJ_SPLIT * nf * nq * RCD; }
 
-// zst rows of the three-launch path ([B][nq][T][8]) or the fused path's stage hand-off rows
-// ([B][nq][FU_NP][FU_ROWS][8]): the workspace holds the larger
+// zst rows of the three-launch path ([B][nq][T][8] floats) or the fused path's tagged stage
+// granules ([B][nq][FU_NP][FU_ROWS][8] x 8 B): the workspace holds the larger
 size_t zst_floats(int batch, int frames, int nq) {
   const size_t a = (size_t)batch * frames * nq * RCD;
-  const size_t b = (size_t)batch * nq * FU_NP * FU_ROWS * RCD;
+  const size_t b = (size_t)batch * nq * FU_NP * FU_ROWS * RCD * 2;
   return a > b ? a : b;
 }
 
@@ -1433,6 +1503,31 @@ int fused_clip_capacity(size_t lds) {
 
 constexpr int FUSED_NA = -1;  // the fused launch does not apply: take the three launches
 
+// Launch timing (vrvq_rvq_timing): while on, every fused launch carries a (start, stop) pair of
+// HIP events in its own dispatch packet (hipExtLaunchKernelGGL), so the elapsed time is the
+// kernel's own duration on its stream (what rocprofv3 reports for it), with no marker packets
+// of their own around it. vrvq_rvq_timing_read averages the recorded pairs.
+struct LaunchTimer {
+  std::mutex mu;
+  bool on = false;
+  std::vector<hipEvent_t> pool;  // 2 per recorded launch
+  size_t used = 0;
+  bool next(hipEvent_t* start, hipEvent_t* stop) {
+    std::lock_guard<std::mutex> guard(mu);
+    if (!on) return false;
+    while (pool.size() < used + 2) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return false;
+      pool.push_back(e);
+    }
+    *start = pool[used];
+    *stop = pool[used + 1];
+    used += 2;
+    return true;
+  }
+};
+LaunchTimer g_timer;
+
 template <int NM, bool PJ3>
 int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* z,
                     const float* imp, int64_t* codes, float* latents, float* loss_pf,
@@ -1450,8 +1545,9 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
     if (e != hipSuccess) return (int)e;
   }
   const int bc_max = min(batch, cap);
-  float* part = ws;
-  float* zsh = ws + part_floats((long long)bc_max * frames, nq);
+  float* part = ws;  // tagged granules: 2 floats per partial
+  unsigned long long* zsh =
+      reinterpret_cast<unsigned long long*>(ws + 2 * part_floats((long long)bc_max * frames, nq));
   const size_t DT = (size_t)RD * frames;
   for (int b0 = 0; b0 < batch; b0 += bc_max) {
     const int bc = min(bc_max, batch - b0);
@@ -1478,10 +1574,23 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
     f.z_q_is = z_q_is ? z_q_is + (size_t)b0 * nq * DT : nullptr;
     f.z_q = z_q + b0 * DT;
     f.zsh = zsh;
-    f.zsh_bytes = (int)((size_t)bc * nq * FU_NP * FU_ROWS * RCD * sizeof(float));
+    f.zsh_bytes = (int)((size_t)bc * nq * FU_NP * FU_ROWS * RCD * 8);
+    if (f.epoch == 1) {
+      // captured launch: every replay carries epoch 1, so the previous replay's granules would
+      // pass the tag checks -- zero them first (memset nodes of the graph)
+      if (hipMemsetAsync(zsh, 0, (size_t)f.zsh_bytes, st) != hipSuccess ||
+          hipMemsetAsync(part, 0, 2 * part_floats((long long)bc * frames, nq) * sizeof(float),
+                         st) != hipSuccess)
+        return VRVQ_ERR_ARG;
+    }
     f.stamps = g_fstamps;
-    hipLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)), dim3(CH_NT),
-                       lds, st, f);
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (g_timer.next(&ev0, &ev1))
+      hipExtLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
+                            dim3(CH_NT), lds, st, ev0, ev1, 0, f);
+    else
+      hipLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
+                         dim3(CH_NT), lds, st, f);
     const int rc = vrvq_launch_status();
     if (rc) return rc;
   }
@@ -1583,7 +1692,8 @@ extern "C" int vrvq_rvq_expand_masked(const float* zst, int batch, int dim, int 
 extern "C" int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes) {
   VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0);
   const long long nf = (long long)batch * frames;
-  *bytes = (long long)(part_floats(nf, nq) + zst_floats(batch, frames, nq)) *
+  // the fused path's partials are tagged granules (2 floats each)
+  *bytes = (long long)(2 * part_floats(nf, nq) + zst_floats(batch, frames, nq)) *
            (long long)sizeof(float);
   return 0;
 }
@@ -1593,6 +1703,32 @@ extern "C" int vrvq_rvq_path(int path) {
   if (path == 1 || path == 2) g_rvq_path = path;
   else if (path != 0) return VRVQ_ERR_ARG;
   return prev;
+}
+
+extern "C" int vrvq_rvq_timing(int on) {
+  std::lock_guard<std::mutex> guard(g_timer.mu);
+  const int prev = g_timer.on ? 1 : 0;
+  g_timer.on = on != 0;
+  return prev;
+}
+
+extern "C" int vrvq_rvq_timing_read(float* mean_ms, int* count) {
+  VRVQ_CHECK_ARG(mean_ms && count);
+  std::lock_guard<std::mutex> guard(g_timer.mu);
+  *mean_ms = 0.0f;
+  *count = 0;
+  double sum = 0.0;
+  for (size_t k = 0; k + 1 < g_timer.used; k += 2) {
+    hipError_t e = hipEventSynchronize(g_timer.pool[k + 1]);
+    float ms = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, g_timer.pool[k], g_timer.pool[k + 1]);
+    if (e != hipSuccess) return (int)e;
+    sum += ms;
+    ++*count;
+  }
+  if (*count) *mean_ms = (float)(sum / *count);
+  g_timer.used = 0;
+  return 0;
 }
 
 extern "C" int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code) {

@@ -601,6 +601,16 @@ std::tuple<Tensor, Tensor> unpack_codes(const Tensor& packed, const Tensor& coun
 // Backward operators of the generator (scripts/train.py:262-330), used by
 // the torch.autograd.Functions of vrvq_amd/train.py.
 
+// Strided weight gradients through the phase-split view (default) | VRVQ_WGRAD_PHASE=0: the
+// strided fp32 weight-gradient kernel.
+static bool phase_wgrad_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("VRVQ_WGRAD_PHASE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // torch.nn.grad.conv1d_weight of a Snake-fused conv (include/vrvq.h, vrvq_conv1d_wgrad).
 Tensor conv1d_wgrad(const Tensor& a, const Tensor& x, int64_t k, int64_t stride, int64_t pad,
                     int64_t dil, const optional<Tensor>& alpha_a,
@@ -625,6 +635,38 @@ Tensor conv1d_wgrad(const Tensor& a, const Tensor& x, int64_t k, int64_t stride,
   // values): the wgrad kernels would otherwise evaluate it in every row tile x chunk that
   // stages the operand (M / 64 times over for x)
   Tensor as_, xs_;
+  if (stride > 1 && (stride & (stride - 1)) == 0 && k == 2 * stride && dil == 1 &&
+      phase_wgrad_enabled()) {
+    // strided taps j = q s + r (the strided encoder convs, the ConvTranspose layers): a stride-1
+    // 2-tap product over the phase-split view xv[c s + r][m] = snake(x)[c][m s + r - pad]
+    // (vrvq_phase_split, Snake applied there), on the x3 weight-gradient kernel; then
+    // dW[m][c][q s + r] = dW'[m][c s + r][q]
+    if (alpha_a.has_value()) {
+      as_ = at::empty_like(a);
+      check_rc(vrvq_snake(a.data_ptr<float>(), (int)B, (int)M, (int)TA, alpha_a->data_ptr<float>(),
+                          inv_alpha_a->data_ptr<float>(), as_.data_ptr<float>(), stream_of(a)),
+               "vrvq_snake");
+    }
+    const int64_t TV = TA + 1, CV = C * stride;
+    Tensor xv = empty_f({B, CV, TV}, a);
+    check_rc(vrvq_phase_split(x.data_ptr<float>(), (int)B, (int)C, (int)TX, (int)stride, (int)pad,
+                              (int)TV, alpha.has_value() ? alpha->data_ptr<float>() : nullptr,
+                              alpha.has_value() ? inv_alpha->data_ptr<float>() : nullptr,
+                              xv.data_ptr<float>(), stream_of(a)),
+             "vrvq_phase_split");
+    int split = 0;
+    long long bytes = 0;
+    check_rc(vrvq_wgrad_plan((int)B, (int)M, (int)TA, (int)CV, 2, &split, &bytes), "vrvq_wgrad_plan");
+    Tensor ws = empty_f({(bytes + 3) / 4}, a);
+    Tensor outv = empty_f({M, CV, 2}, a);
+    check_rc(vrvq_conv1d_wgrad(alpha_a.has_value() ? as_.data_ptr<float>() : a.data_ptr<float>(),
+                               (int)B, (int)M, (int)TA, nullptr, nullptr, xv.data_ptr<float>(),
+                               (int)CV, (int)TV, nullptr, nullptr, 2, 1, 0, 1, split,
+                               ws.data_ptr<float>(), (long long)ws.numel() * 4,
+                               outv.data_ptr<float>(), stream_of(a)),
+             "vrvq_conv1d_wgrad");
+    return outv.view({M, C, stride, 2}).permute({0, 1, 3, 2}).reshape({M, C, k}).contiguous();
+  }
   if (alpha_a.has_value()) {
     as_ = at::empty_like(a);
     check_rc(vrvq_snake(a.data_ptr<float>(), (int)B, (int)M, (int)TA, alpha_a->data_ptr<float>(),
