@@ -107,7 +107,8 @@ def main():
         m(torch.zeros(args.batch, 1, 44100), 44100, None, 1.0)
     rows = list(csv.DictReader(open(args.trace)))
     conv = [r for r in rows if any(k in r["Kernel_Name"] for k in
-                                   ("conv_mfma_kernel", "conv_small", "conv_cout1", "ru_fused_kernel"))]
+                                   ("conv_mfma_kernel", "conv_small", "conv_cout1", "conv_cin1",
+                                    "ru_fused_kernel"))]
     step = conv[-len(CALLS):]
     tot_t = tot_f = 0.0
     # %pk against the ceiling of the path the kernel runs: the x3 split-bf16 MFMA (template
@@ -118,7 +119,7 @@ def main():
         kn = r["Kernel_Name"]
         i = kn.find("<")
         pre = ("mfma" if "mfma" in kn else "ru" if "ru_fused" in kn else
-               "cout1" if "cout1" in kn else "small")
+               "cout1" if "cout1" in kn else "cin1" if "cin1" in kn else "small")
         targs = [t.strip() for t in kn[i + 1:kn.find(">")].split(",")] if i >= 0 else []
         # conv_mfma_kernel<BM, BN, WM, NW, KS, X3[, PH]>, ru_fused_kernel<C, BN, WM, NW, X3>
         x3 = ((pre == "mfma" and len(targs) >= 6 and targs[5] == "true") or

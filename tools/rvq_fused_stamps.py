@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--nq", type=int, default=8)
     ap.add_argument("--frames", type=int, default=87)
+    ap.add_argument("--no-zqis", action="store_true",
+                    help="z_q_is not materialised (the expansion writes z_q only)")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", "libvrvq_hip_stamps.so"))
     lib.vrvq_rvq_path.restype = ctypes.c_int
@@ -61,7 +63,8 @@ def main():
         rc = lib.vrvq_rvq_encode(P(z), B, 1024, T, nq, 1024, 8, P(st.w_in_t), P(st.b_in),
                                  P(st.cb), P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
                                  P(st.mcol), P(st.qb), P(imp), ctypes.c_float(1.0), P(codes),
-                                 P(lat), P(loss), P(zqis), P(zq), P(mask), P(ws),
+                                 P(lat), P(loss), None if args.no_zqis else P(zqis), P(zq),
+                                 P(mask), P(ws),
                                  ctypes.c_longlong(ws.numel() * 4), stream)
         assert rc == 0, rc
 
@@ -72,6 +75,8 @@ def main():
     ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
     assert torch.equal(ref[0], codes), "stamped build disagrees with the product library"
     assert torch.equal(ref[4], zq), "stamped build disagrees with the product library"
+    if args.no_zqis:
+        print("z_q_is not materialised")
     s = stamps.cpu().numpy().reshape(grid, 64).astype(np.int64)
     t0 = s[:, 0].min()
     us = lambda v: (v - t0) / 100.0  # noqa: E731

@@ -489,21 +489,30 @@ __device__ __forceinline__ void project3_body(const float* __restrict__ z, int T
       for (int u = 0; u < 4; ++u) rvq_split3x2(w[ks][2 * u], w[ks][2 * u + 1], h[u], mm[u], l[u]);
       const u32x4 ah = {h[0], h[1], h[2], h[3]}, am = {mm[0], mm[1], mm[2], mm[3]},
                   al = {l[0], l[1], l[2], l[3]};
+      // the three column tiles' products interleaved (three independent accumulators: the
+      // matrix core is not left waiting on a dependent MFMA); per tile the order stays
+      // m m, h l, l h, h m, m h, h h
+      u32x4 bh[3], bm[3], bl[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const char* bp = lds + ((3 * hf + j) * 16 + lr) * (PJ3_LDB * 2) + (32 * ks + 8 * kg) * 2;
-        const u32x4 bh = *reinterpret_cast<const u32x4*>(bp);
-        const u32x4 bm = *reinterpret_cast<const u32x4*>(bp + PJ3_PLANE);
-        const u32x4 bl = *reinterpret_cast<const u32x4*>(bp + 2 * PJ3_PLANE);
-        __builtin_amdgcn_sched_barrier(0);  // one tile's operands live at a time
-        f32x4 c = acc[j];
-        c = mfma16_bf16(am, bm, c);  // m m
-        c = mfma16_bf16(ah, bl, c);  // h l
-        c = mfma16_bf16(al, bh, c);  // l h
-        c = mfma16_bf16(ah, bm, c);  // h m
-        c = mfma16_bf16(am, bh, c);  // m h
-        acc[j] = mfma16_bf16(ah, bh, c);  // h h
+        bh[j] = *reinterpret_cast<const u32x4*>(bp);
+        bm[j] = *reinterpret_cast<const u32x4*>(bp + PJ3_PLANE);
+        bl[j] = *reinterpret_cast<const u32x4*>(bp + 2 * PJ3_PLANE);
       }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(am, bm[j], acc[j]);  // m m
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(ah, bl[j], acc[j]);  // h l
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(al, bh[j], acc[j]);  // l h
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(ah, bm[j], acc[j]);  // h m
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(am, bh[j], acc[j]);  // m h
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = mfma16_bf16(ah, bh[j], acc[j]);  // h h
+      __builtin_amdgcn_sched_barrier(0);  // one K step's operands live at a time
     }
     // D layout: lane l, reg q -> row 4 (l >> 4) + q of the tile, frame l & 15
     const int rr = rt * 16 + 4 * kg;  // rows rr..rr+3 all valid iff rr < R (R = 8 nq)
