@@ -509,6 +509,17 @@ static int conv_x3_wide() {
   return v;
 }
 
+// 2-tap GEMMs at T < 4096 that the padding rule sends to 64-wide tiles: tuning override
+// VRVQ_CONV_PH128=1 (the strided encoder convs through the phase-split view on 128-wide pair
+// tiles: half the weight re-streaming) | 2 (also the ConvTranspose layers) | 0 (default)
+static int conv_ph128() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_PH128");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -528,6 +539,9 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     bn = 64;
   else if (a.ng < 4096 && conv_bn_rule() == 1 && waste(128) * 100 > a.ng * 15) bn = 64;
   else bn = 128;
+  if (KS == 2 && bn == 64 && a.w3 != nullptr &&
+      ((a.psh > 0 && conv_ph128() >= 1) || (a.up > 0 && conv_ph128() >= 2)))
+    bn = 128;
   if (KS == 2 && a.up > 0 && 128 % a.up != 0) {
     // polyphase ConvTranspose1d with a stride that does not divide 128 (3, 6): 192-row tiles,
     // which hold whole output channels; other strides (5, 7, ...) are rejected by launch_cfg
