@@ -11,6 +11,6 @@ run() { local name=$1 to=$2; shift 2
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; return 0; }
 run bench 300 python bench.py --batch 64 --n-codebooks 32 --steps 10 --warmup 3 --no-cpu-baseline
 run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py --batch 64 --n-codebooks 32 --steps 3 --warmup 2 --no-cpu-baseline
-run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/rvqprof_$T -o run --output-format csv -- python tools/rvq_bench.py --batch 64 --nq 32 --iters 20
-TAG=${T} RVQ_ARGS="--batch 64 --nq 32" bash tools/gpu/pmc_rvq.sh || exit 1
+run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/rvqprof_$T -o run --output-format csv -- python tools/rvq_bench.py --batch 64 --nq 32 --iters 20 --paths 2 --variants 3
+TAG=${T} PER_CALL=2 RVQ_ARGS="--batch 64 --nq 32 --paths 2 --variants 3" bash tools/gpu/pmc_rvq.sh || exit 1
 exit 0

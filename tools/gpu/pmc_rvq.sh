@@ -10,5 +10,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 90 rocprofv3 --pmc $c --kernel-include-regex "rvq_" -d gpurun_out/${TAG}_$c -o run --output-format csv -- python tools/rvq_bench.py --iters 10 ${RVQ_ARGS} > gpurun_out/${TAG}_$c.log 2>&1
   rc=$?; echo "rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-python tools/pmc_traffic.py gpurun_out/${TAG} gpurun_out/${TAG}_rvq_pmc.json
+python tools/pmc_traffic.py gpurun_out/${TAG} gpurun_out/${TAG}_rvq_pmc.json ${PER_CALL:-1}
 exit 0

@@ -12,16 +12,14 @@ run() { local name=$1 to=$2; shift 2
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi; return 0; }
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 PT="python -u -m pytest -x -q -rf --timeout 120 --timeout-method thread"
+has smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has fused && run fused_tests 300 $PT tests/test_gpu_parity.py -k "rvq_fused"
 has rvqb && run rvq_b32 120 python tools/rvq_bench.py --batch 32 --nq 8
 has rvqb && run rvq_b64 120 python tools/rvq_bench.py --batch 64 --nq 32
 has stamps && TAIL=40 run stamps 120 python tools/rvq_fused_stamps.py
 has nozqis && TAIL=40 run stamps_nozqis 120 python tools/rvq_fused_stamps.py --no-zqis
-has latepub && run rvq_b32_lp0 120 env VRVQ_RVQ_LATEPUB=0 python tools/rvq_bench.py --batch 32 --nq 8 --paths 2 --variants 3
-has latepub && run rvq_b64_lp0 120 env VRVQ_RVQ_LATEPUB=0 python tools/rvq_bench.py --batch 64 --nq 32 --paths 2 --variants 3
-has exsleep && for n in 4 16; do run rvq_b32_sl$n 120 env VRVQ_RVQ_EXSLEEP=$n python tools/rvq_bench.py --batch 32 --nq 8 --paths 2 --variants 3; done
-has exsleep && TAIL=40 run stamps_sl16 120 env VRVQ_RVQ_EXSLEEP=16 python tools/rvq_fused_stamps.py
 has conv && run conv_tests 400 $PT tests/test_gpu_parity.py -k "conv or strided or transpose"
+has benchfull && run benchfull 400 python bench.py
 has bench && run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 has sweep && run sweep 300 python bench.py --sweep --steps 10 --warmup 2 --no-cpu-baseline
 has cfg3 && run cfg3 300 python bench.py --batch 64 --n-codebooks 32 --steps 10 --warmup 2 --no-cpu-baseline
@@ -31,6 +29,7 @@ has knob && run bench_ph1 300 env VRVQ_CONV_PH128=1 python bench.py --steps 20 -
 has knob && run bench_ph2 300 env VRVQ_CONV_PH128=2 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 has knobprof && run prof_ph 300 env VRVQ_CONV_PH128=2 VRVQ_CONV_BN96_MIN=200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_ph -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 has rvqprof && run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_rvq -o run --output-format csv -- python tools/rvq_bench.py --batch 32 --nq 8 --iters 20 --paths 2 --variants 3
+has pmcrvq && run pmcrvq 300 env TAG=${TAG} RVQ_ARGS="--batch 32 --nq 8 --paths 2 --variants 3" bash tools/gpu/pmc_rvq.sh
 has prof && run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 has train && run train_tests 400 $PT tests/test_gpu_train.py -k "wgrad or snake_conv_grads or golden"
 has all && run gpu_tests 900 $PT tests -m gpu

@@ -8,7 +8,10 @@ a wide coalesced streaming read, so the fetch bytes are doubled; WRITE_SIZE is e
 16-B-per-lane streaming stores (the expansion's stores are 4-B-per-lane rows: uncalibrated,
 reported as read).
 
-    python tools/pmc_traffic.py gpurun_out/<tag> profiles/<tag>_rvq_pmc.json
+    python tools/pmc_traffic.py gpurun_out/<tag> profiles/<tag>_rvq_pmc.json [launches per call]
+
+The path is rvq_fused_kernel where the fused launch ran (one dispatch per <= 32 clips: the
+third argument, default 1, scales a dispatch to one rvq_encode call), else the three kernels.
 """
 import collections
 import csv
@@ -30,6 +33,7 @@ def per_kernel(root, counter):
 
 def main():
     root, out = sys.argv[1], sys.argv[2]
+    per_call = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
     fetch = per_kernel(root, "FETCH_SIZE")
     write = per_kernel(root, "WRITE_SIZE")
     kernels = {}
@@ -38,13 +42,22 @@ def main():
         kernels[k] = {"fetch_size_kib": f_kib, "write_size_kib": w_kib,
                       "fetch_bytes_corrected": 2 * f_kib * 1024, "write_bytes": w_kib * 1024,
                       "total": 2 * f_kib * 1024 + w_kib * 1024}
-    path = [k for k in kernels if any(s in k for s in ("rvq_project", "rvq_chain", "rvq_expand"))]
+    if "rvq_fused_kernel" in kernels:
+        path = ["rvq_fused_kernel"]
+    else:
+        path = [k for k in kernels
+                if any(s in k for s in ("rvq_project", "rvq_chain", "rvq_expand"))]
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                     "python tools/rvq_bench.py (B=32, nq=8), kernel-trace only",
+                     "python tools/rvq_bench.py, kernel-trace only",
            "fetch_correction": "x2 (MI355X_MICROARCH.md: gfx950 FETCH_SIZE = half the bytes "
                                "of wide coalesced reads)",
            "kernels": kernels,
-           "path_total_bytes": sum(kernels[k]["total"] for k in path)}
+           "path": path,
+           "launches_per_call": per_call,
+           "path_total_bytes": per_call * sum(kernels[k]["total"] for k in path),
+           "path_total_bytes_uncorrected": per_call * sum(
+               1024 * (kernels[k]["fetch_size_kib"] + kernels[k]["write_size_kib"])
+               for k in path)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

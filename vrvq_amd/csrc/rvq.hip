@@ -656,7 +656,6 @@ struct ChainHandoff {              // fused launch only
   __amdgpu_buffer_rsrc_t part;     // the partials' tagged granules, read with sc1 loads
   unsigned long long* zsh;         // this part's stage-0 block of tagged zst granules
   int zsh_stage;                   // granules per stage
-  int late_pub;                    // publish stage i's granules behind stage i+1's gather
   unsigned long long* stamps;      // diagnostic build only
 };
 
@@ -803,10 +802,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
                          g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
-  // late_pub: stage i's store is issued in stage i+1 right behind the candidate-row gather, so
-  // the gather's wait (vmcnt retires in order) does not include a write-through store
-  float pub_v = 0.0f;
-  int pub_i = -1;
   for (int i = 0; i < nq; ++i) {
     const bool more = i + 1 < nq;
     // ---- S1 ----
@@ -905,11 +900,6 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
       const float* row = a.cb + ((size_t)i * N + (lane < nf ? bidx : 0)) * RCD;
       const float4 r0 = ld4(row), r1 = ld4(row + 4);
       __builtin_amdgcn_sched_barrier(0);  // keep the gather ahead of the prefetch (vmcnt order)
-      if constexpr (FUSED) {
-        if (pub_i >= 0) publish(pub_i, pub_v);
-        pub_i = -1;
-        __builtin_amdgcn_sched_barrier(0);
-      }
       {  // stage i+1 operands (cbn fragments, c2 slice, M column). Unconditional loads from
          // clamped addresses (the last stage re-reads its own): a branch around them makes the
          // waitcnt pass assume none are outstanding at the join, so the candidate-row wait
@@ -957,14 +947,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
       zq = cr_s[(rf * CH_NW + bw) * RCD + rk];  // raw codebook row of the winner
     }
     const float zsv = ze + (zq - ze);  // z_e + (z_q - z_e).detach(), models/quantize.py:73-75
-    if constexpr (FUSED) {
-      if (hx.late_pub && more) {
-        pub_v = zsv;
-        pub_i = i;
-      } else {
-        publish(i, zsv);
-      }
-    }
+    if constexpr (FUSED) publish(i, zsv);
     const float diff = ze - zq;
     const float l2 = vrvq::sum8(diff * diff, lane);
     if (role) {
@@ -1154,8 +1137,6 @@ struct FusedArgs {
   int zsh_bytes;
   unsigned* sync;
   unsigned epoch;
-  int exsleep;                      // expansion re-read interval, s_sleep(4) units (A/B knob)
-  int late_pub;                     // ChainHandoff::late_pub (VRVQ_RVQ_LATEPUB, default 1)
   unsigned long long* stamps;       // diagnostic build only
 };
 
@@ -1259,7 +1240,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
         dead = true;
         break;
       }
-      for (int k = 0; k < f.exsleep; ++k) __builtin_amdgcn_s_sleep(4);
+      __builtin_amdgcn_s_sleep(4);
       load_z(i, cur.z);
     }
     FSTAMP(f.stamps, 1 + i);
@@ -1336,7 +1317,6 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   hx.part = pr;
   hx.zsh = f.zsh + (size_t)(b * nq * FU_NP + s) * FU_ROWS * RCD;
   hx.zsh_stage = FU_NP * FU_ROWS * RCD;
-  hx.late_pub = f.late_pub;
   hx.stamps = f.stamps;
   chain_body<NM, true>(f.c, sm, b * T + s * F, nf, hx);
 }
@@ -1557,26 +1537,6 @@ struct LaunchTimer {
 };
 LaunchTimer g_timer;
 
-int g_exsleep = -1;  // VRVQ_RVQ_EXSLEEP (A/B knob), read once
-
-int fused_exsleep() {
-  if (g_exsleep < 0) {
-    const char* e = getenv("VRVQ_RVQ_EXSLEEP");
-    g_exsleep = e ? max(1, atoi(e)) : 1;
-  }
-  return g_exsleep;
-}
-
-int g_late_pub = -1;  // VRVQ_RVQ_LATEPUB (A/B knob), read once
-
-int fused_late_pub() {
-  if (g_late_pub < 0) {
-    const char* e = getenv("VRVQ_RVQ_LATEPUB");
-    g_late_pub = e ? (atoi(e) != 0) : 1;
-  }
-  return g_late_pub;
-}
-
 template <int NM, bool PJ3>
 int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* z,
                     const float* imp, int64_t* codes, float* latents, float* loss_pf,
@@ -1633,8 +1593,6 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
         return VRVQ_ERR_ARG;
     }
     f.stamps = g_fstamps;
-    f.exsleep = fused_exsleep();
-    f.late_pub = fused_late_pub();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (g_timer.next(&ev0, &ev1))
       hipExtLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
