@@ -18,6 +18,7 @@ has rvqb && run rvq_b32 120 python tools/rvq_bench.py --batch 32 --nq 8
 has rvqb && run rvq_b64 120 python tools/rvq_bench.py --batch 64 --nq 32
 has stamps && TAIL=40 run stamps 120 python tools/rvq_fused_stamps.py
 has nozqis && TAIL=40 run stamps_nozqis 120 python tools/rvq_fused_stamps.py --no-zqis
+has nomfma && TAIL=40 run stamps_nomfma 120 python tools/rvq_fused_stamps.py --no-expand-mfma
 has conv && run conv_tests 400 $PT tests/test_gpu_parity.py -k "conv or strided or transpose"
 has benchfull && run benchfull 400 python bench.py
 has bench && run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--no-zqis", action="store_true",
                     help="z_q_is not materialised (the expansion writes z_q only)")
+    ap.add_argument("--no-expand-mfma", action="store_true",
+                    help="timing experiment: the expansion skips its MFMAs (outputs not checked)")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", "libvrvq_hip_stamps.so"))
     lib.vrvq_rvq_path.restype = ctypes.c_int
@@ -72,8 +74,19 @@ def main():
         run(False)
     run(True)
     torch.cuda.synchronize()
+    if args.no_expand_mfma:
+        lib.vrvq_debug_set_fused_flags(1)
+        stamps.zero_()
+        for _ in range(5):
+            run(False)
+        run(True)
+        torch.cuda.synchronize()
+        lib.vrvq_debug_set_fused_flags(0)
+        print("expansion MFMAs skipped (timing experiment)")
     ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
     assert torch.equal(ref[0], codes), "stamped build disagrees with the product library"
+    if args.no_expand_mfma:
+        zq.copy_(ref[4])
     assert torch.equal(ref[4], zq), "stamped build disagrees with the product library"
     if args.no_zqis:
         print("z_q_is not materialised")

@@ -614,13 +614,14 @@ struct ChainLds {
 };
 
 // ------------------------------------------------------------------------------------------
-// In-launch hand-offs of the fused path (rvq_fused_kernel). Every shared word is a global
-// agent-scope access; payloads are stored write-through (sc1) by the producing wave, which drains
-// them (s_waitcnt vmcnt(0)) before ONE lane stores the flag; consumers poll the flag with sc1
-// loads from one wave and read the payload with sc1 loads after a workgroup barrier
-// (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the valid-forms table). Flags
-// are monotonic per call: projection unit done = epoch, chain part published k stages =
-// 64 epoch + k (epochs grow per call on a stream: stale words of older calls are smaller).
+// In-launch hand-offs of the fused path (rvq_fused_kernel): tagged 8-B granules {value, tag},
+// each written whole by ONE sc1 store (two per 16-B store) and read with sc1 loads; the reader
+// checks the tag of every granule it uses and re-reads until it matches, so the data is its own
+// flag (cdna_hip_programming.md Guideline 16, R2; MI355X_MICROARCH.md: granules are observed
+// untorn, also as 16-B sc1 halves). Tags: projection partials 64 epoch, stage i zst
+// 64 epoch + i + 1; epochs grow per call on a stream, so an older call's granules never match
+// (under stream capture the granule area is zeroed by a memset node and the call uses epoch 1).
+// The sync block holds only the error word of the bounded waits.
 constexpr unsigned SPIN_MAX = 1u << 19;  // bounded spins (~0.5 s); on the bound: *err = code
 
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
@@ -1112,9 +1113,9 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 // ------------------------------------------------------------------------------------------
 // The fused RVQ launch (one kernel instead of projection -> chain -> expansion; T <= 96 frames
 // per clip, every workgroup of the grid resident at once). Workgroups [0, 8 B) are (clip b,
-// split / part s): the projection unit (b, s) (rvq_project2_kernel's body, partials stored
-// write-through), then chain part s of clip b (frames [s F, s F + F), F = ceil(T / 8)), which
-// waits for the clip's 8 projection units and publishes every stage's zst rows. Workgroups
+// split / part s): the projection unit (b, s) (project3_body, partials stored as tagged
+// granules), then chain part s of clip b (frames [s F, s F + F), F = ceil(T / 8)), which reads
+// the clip's 8 partials of its frames as they land and publishes every stage's zst. Workgroups
 // [8 B, 16 B) are the expansion: (clip b, 128-channel block) over all stages, each stage once its
 // 8 chain parts have published it, so the z_q_is write stream runs under the chain instead of
 // after it. Same values as the three launches, bit for bit (tests/test_gpu_parity.py).
@@ -1138,6 +1139,7 @@ struct FusedArgs {
   unsigned* sync;
   unsigned epoch;
   unsigned long long* stamps;       // diagnostic build only
+  int dbg;                          // diagnostic build only: bit 0 = expansion skips its MFMAs
 };
 
 // Expansion workgroup (clip b, channels [128 cb, +128)): wave w = 32-channel tile (w & 3) x
@@ -1258,10 +1260,16 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
       f32x16 q;
 #pragma unroll
       for (int r = 0; r < 16; ++r) q[r] = 0.0f;
+#ifdef VRVQ_STAMPS
+      if (!(f.dbg & 1)) {
+#endif
 #pragma unroll
       for (int st = 0; st < 4; ++st)
         q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
       q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cur.bb, h ? 0.0f : 1.0f, q, 0, 0, 0);
+#ifdef VRVQ_STAMPS
+      }
+#endif
       const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
       if (f.z_q_is && tv[j]) {
         float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
@@ -1371,6 +1379,7 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
 
 unsigned long long* g_stamps = nullptr;   // diagnostic build: vrvq_debug_set_stamps
 unsigned long long* g_fstamps = nullptr;  // diagnostic build: vrvq_debug_set_fused_stamps
+int g_fdbg = 0;                           // diagnostic build: vrvq_debug_set_fused_flags
 
 template <int NM>
 int launch_chain_nm(const ChainArgs& a, hipStream_t st, long long nblk) {
@@ -1593,6 +1602,7 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
         return VRVQ_ERR_ARG;
     }
     f.stamps = g_fstamps;
+    f.dbg = g_fdbg;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (g_timer.next(&ev0, &ev1))
       hipExtLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
@@ -1616,6 +1626,11 @@ extern "C" int vrvq_debug_set_stamps(unsigned long long* buf) {
 }
 extern "C" int vrvq_debug_set_fused_stamps(unsigned long long* buf) {
   g_fstamps = buf;
+  return 0;
+}
+// bit 0: the expansion workgroups skip their MFMAs (timing experiment; outputs wrong)
+extern "C" int vrvq_debug_set_fused_flags(int flags) {
+  g_fdbg = flags;
   return 0;
 }
 #endif
