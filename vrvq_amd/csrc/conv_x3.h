@@ -328,14 +328,6 @@ __device__ __forceinline__ void conv_mainloop_x3(
       __syncthreads();
     }
   }
-  // k = 1 tiles on one stage: the next chunk's loads are issued BEFORE the chunk's MFMAs
-  // (their registers fit beside the k = 1 operands: 32 channels x the window, one tap), so the
-  // memory latency runs under the MFMAs instead of between the two barriers
-#ifdef VRVQ_X3_NO_PF1  // A/B build (the refill between the barriers, as before r04)
-  constexpr bool PF1 = false;
-#else
-  constexpr bool PF1 = X3_STAGES == 1 && KS == 1;
-#endif
   int cur = 0;
   load_w(0);
   load_x(0);
@@ -348,7 +340,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
     // the MFMAs into the store block, their only user.
     const int cn = min(c + 1, nchunks - 1);
     char* nxt = sbase + (cur ^ (X3_STAGES - 1)) * STG;
-    if constexpr (X3_STAGES == 2 || PF1) {
+    if constexpr (X3_STAGES == 2) {
       load_w(cn);
       load_x(cn * CK);
       __builtin_amdgcn_sched_barrier(0);
@@ -358,12 +350,13 @@ __device__ __forceinline__ void conv_mainloop_x3(
     if constexpr (X3_STAGES == 1) {
       // Single stage: the refill is not prefetched (its registers would coexist with the
       // MFMA operands and spill); the other workgroup on the CU runs its MFMAs meanwhile.
+      // Measured on the k = 1 tiles, where the prefetch registers do fit (r04p,
+      // profiles/r04p_k1_prefetch_ab.txt): 2-23 % slower per layer -- the 128 x 64 tile drops
+      // from three workgroups per CU to two, the 128 x 128 one gains nothing.
       __syncthreads();  // every wave done with the stage
       if (c + 1 < nchunks) {
-        if constexpr (!PF1) {
-          load_w(cn);
-          load_x(cn * CK);
-        }
+        load_w(cn);
+        load_x(cn * CK);
         // every load of the refill in flight before the first store waits on one (else the
         // x loads are issued only after the W stores: two memory round trips per chunk)
         __builtin_amdgcn_sched_barrier(0);
