@@ -53,7 +53,12 @@ void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TC::RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR>(a, smem, acc, b, m0, n0);
+#ifdef VRVQ_X3_SB_CONV
+  constexpr bool SB = KS == 1 || (KS == 2 && BN == 128);  // A/B build
+#else
+  constexpr bool SB = false;
+#endif
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
   else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
 }

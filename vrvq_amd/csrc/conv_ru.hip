@@ -64,7 +64,12 @@ void ru_fused_kernel(RuArgs ra) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   // phase 1 on the bf16x3 split path when a pre-split W7 is given (conv_x3.h)
-  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);
+#ifdef VRVQ_X3_SB_RU
+  constexpr bool SB = BM == 96 || BM == 192 || BM == 128;  // A/B build
+#else
+  constexpr bool SB = false;
+#endif
+  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, 7, false, x3_pair<7, BM, BN>(), SB>(a, smem, acc, b, 0, n0);
   else conv_mainloop<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);  // ends with a barrier
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -237,6 +242,16 @@ static bool ru_x3_ok(int C) {
   return v == 2 ? true : v == 1 ? (C == 64 || C == 128) : false;
 }
 
+// tuning override: VRVQ_RU_BN64=1 runs the C = 64 / 128 units on 64-wide time tiles (more
+// workgroups per CU; C = 128 then fits phase 2 on the x3 MFMA) | 0 (default: 128-wide)
+static bool ru_bn64() {
+  static const bool v = [] {
+    const char* e = getenv("VRVQ_RU_BN64");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 template <int BM, int BN, int WM, int NW>
 int launch_ru(RuArgs ra, int batch, hipStream_t st) {
   constexpr int CK = ChunkCfg<7, BM, BN>::CK;
@@ -315,9 +330,13 @@ extern "C" int vrvq_residual_unit(const float* x, const float* x_snk, int batch,
   ra.C = channels;
   hipStream_t st = as_stream(stream);
   switch (channels) {
-    case 64: return launch_ru<64, 128, 2, 4>(ra, batch, st);
+    case 64:
+      if (ru_bn64()) return launch_ru<64, 64, 2, 4>(ra, batch, st);
+      return launch_ru<64, 128, 2, 4>(ra, batch, st);
     case 96: return launch_ru<96, 128, 1, 4>(ra, batch, st);
-    case 128: return launch_ru<128, 128, 2, 4>(ra, batch, st);
+    case 128:
+      if (ru_bn64()) return launch_ru<128, 64, 2, 4>(ra, batch, st);
+      return launch_ru<128, 128, 2, 4>(ra, batch, st);
     case 192: return launch_ru<192, 64, 2, 4>(ra, batch, st);
     case 256: return launch_ru<256, 64, 2, 4>(ra, batch, st);
     default: return VRVQ_ERR_UNSUPPORTED;

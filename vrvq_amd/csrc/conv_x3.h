@@ -114,8 +114,10 @@ struct X3W {
 // stride-1 windows only (a.ssh == 0), a.w3 = the pre-split weight.
 // PH: the phase-split view of a strided conv (ConvArgs::psh > 0; compile-time, so the stride-1
 // instantiations keep their plain window addressing).
+// SB: single-buffered LDS operand reads in the chunk's MFMA loop (one step's operands live
+// instead of two: fewer registers, so more workgroups per CU where the registers were the limit)
 template <int BM, int BN, int WM, int NW, int KS, bool PH = false,
-          bool PAIR = x3_pair<KS, BM, BN>()>
+          bool PAIR = x3_pair<KS, BM, BN>(), bool SB = false>
 __device__ __forceinline__ void conv_mainloop_x3(
     const ConvArgs& a, float* smem,
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
@@ -304,6 +306,15 @@ __device__ __forceinline__ void conv_mainloop_x3(
       }
   };
   auto chunk_mma = [&](const u32x4* ws, const u32x4* xs) {
+    if constexpr (SB) {
+#pragma unroll
+      for (int q = 0; q < NSTEP; ++q) {
+        u32x4 a0[3][RM], b0[3][RN];
+        rd_at(ws, xs, q, a0, b0);
+        mma_at(a0, b0);
+      }
+      return;
+    }
     u32x4 a0[3][RM], b0[3][RN], a1[3][RM], b1[3][RN];
     rd_at(ws, xs, 0, a0, b0);
 #pragma unroll
