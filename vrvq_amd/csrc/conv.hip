@@ -53,10 +53,12 @@ void conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TC::RN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-#ifdef VRVQ_X3_SB_CONV
-  constexpr bool SB = KS == 1 || (KS == 2 && BN == 128);  // A/B build
+  // single-buffered operand reads (conv_x3.h) on the k1 and 128-wide 2-tap tiles: 2-6 % per
+  // k1 layer, +1.7 % end to end with the ResidualUnit rule (profiles/r04q_sb_ab.txt)
+#ifdef VRVQ_X3_SB_ALL  // A/B build
+  constexpr bool SB = true;
 #else
-  constexpr bool SB = false;
+  constexpr bool SB = KS == 1 || (KS == 2 && BN == 128);
 #endif
   if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
   else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);

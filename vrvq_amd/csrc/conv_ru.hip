@@ -64,10 +64,12 @@ void ru_fused_kernel(RuArgs ra) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   // phase 1 on the bf16x3 split path when a pre-split W7 is given (conv_x3.h)
-#ifdef VRVQ_X3_SB_RU
-  constexpr bool SB = BM == 96 || BM == 192 || BM == 128;  // A/B build
+  // single-buffered operand reads in phase 1 (conv_x3.h): C = 96 / 128 / 192 units 2-4 %
+  // faster (profiles/r04q_sb_ab.txt; C = 96 drops to 164 VGPRs: three workgroups per CU)
+#ifdef VRVQ_X3_SB_ALL  // A/B build
+  constexpr bool SB = true;
 #else
-  constexpr bool SB = false;
+  constexpr bool SB = BM == 96 || BM == 192 || BM == 128;
 #endif
   if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, 7, false, x3_pair<7, BM, BN>(), SB>(a, smem, acc, b, 0, n0);
   else conv_mainloop<BM, BN, WM, NW, 7>(a, smem, acc, b, 0, n0);  // ends with a barrier
