@@ -370,7 +370,9 @@ static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
 // fit (the caller then takes the fp32-input loop).
 template <int BM, int BN, int WM, int NW, int KS, bool PAIR>
 int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t st) {
-  size_t lx = x3_lds_bytes<KS, BM, BN, PAIR>(XW, a.psh ? a.cin >> a.psh : a.cin);
+  // the pair tiles' Snake table only when the staging applies a Snake (the producer-side
+  // snake(x) inputs of the k7 layers need none: 3-6 KB of LDS back)
+  size_t lx = x3_lds_bytes<KS, BM, BN, PAIR>(XW, a.alpha ? (a.psh ? a.cin >> a.psh : a.cin) : 0);
   if (lx < epi) lx = epi;
   if (lx > 160 * 1024) return VRVQ_ERR_UNSUPPORTED;
   if constexpr (KS == 2) {
@@ -560,8 +562,9 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   if constexpr (KS == 7) {
     const int wide = conv_x3_wide();
     if (a.w3 != nullptr && a.stride == 1 && a.up == 0 && a.M >= 128 && a.M % 64 == 0 &&
-        a.cin % 16 == 0 && ((wide >= 1 && a.ng >= 4096) || (wide == 2 && a.ng >= 640)))
+        a.cin % 16 == 0 && ((wide >= 1 && a.ng >= 4096) || (wide == 2 && a.ng >= 640))) {
       return launch_cfg<64, 256, 1, 4, KS>(a, batch, st);
+    }
   }
   if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
   if (bn == 96) return launch_cfg<128, 96, 4, 4, KS>(a, batch, st);
