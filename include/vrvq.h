@@ -240,9 +240,10 @@ int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
 int vrvq_rvq_path(int path);
 
 /* The fused launch's in-kernel waits are bounded: a wait that runs out (a hang averted: it
- * cannot happen with the whole grid resident) records a code in the stream's flag block and the
- * launch runs on with garbage. *code = that code (1 projection wait, 2 stage wait) or 0, and it
- * is cleared. Synchronises the stream. */
+ * cannot happen with the whole grid resident) records a code in the stream's sync block and the
+ * launch runs on with garbage. *code = that code (1: a chain part's wait for the projection
+ * partials, 2: an expansion wait for a stage) or 0, and it is cleared. Synchronises the
+ * stream. */
 int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code);
 
 /* Kernel timing of the fused launch (bench.py's roofline): while on (process-wide), every fused
@@ -258,10 +259,13 @@ int vrvq_rvq_timing_read(float* mean_ms, int* count);
  * ResidualVectorQuantize.forward in eval (:136-214): one fused launch (projection units, chain
  * parts that publish every stage's zst rows, expansion workgroups that write z_q_is / z_q
  * under the chain; see vrvq_rvq_path) or three stream-ordered launches (project -> chain ->
- * expand, the steps below). The fused launches of a stream share a small flag block the library
- * allocates on first use (hipMalloc, outside any stream capture); under stream capture a memset
- * of it is captured in front of each launch. workspace: >= vrvq_rvq_workspace() bytes, 16-byte
- * aligned, caller-owned, no initialisation needed. */
+ * expand, the steps below). The fused launch hands data between its workgroups as tagged 8-byte
+ * granules in the workspace (the tag carries a per-call epoch, so nothing needs clearing
+ * between eager calls); the launches of a stream share a small sync block (the error word) the
+ * library allocates on first use (hipMalloc, outside any stream capture); under stream capture
+ * memsets of it and of the granule areas are captured in front of each launch (every replay
+ * uses the same epoch). workspace: >= vrvq_rvq_workspace() bytes, 16-byte aligned,
+ * caller-owned, no initialisation needed. */
 int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
                     const float* w_in_t, const float* b_in, const float* cb, const float* cbf,
                     const float* c2, const float* w_out, const float* b_out, const float* mcol,
