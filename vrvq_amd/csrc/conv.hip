@@ -529,6 +529,14 @@ static int conv_ph128() {
   return v;
 }
 
+static int conv_k1x3_192() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_K1X3_192");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -604,6 +612,11 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
   if constexpr (KS == 1) {
+    // x3 k1 GEMMs with M a multiple of 192 on 192 x 64 single-buffered tiles (154 VGPRs, three
+    // workgroups per CU; each x column block read 2x / 4x instead of 3x / 6x): tuning override
+    // VRVQ_CONV_K1X3_192=1 | 0 (default)
+    if (conv_k1x3_192() && a.w3 != nullptr && a.M % 192 == 0)
+      return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     // k = 1 GEMMs with M a multiple of 192 (the 384 / 768-channel ResidualUnit k1 + skip):
     // 192-row tiles read each x column block 2x / 4x instead of 3x / 6x (tuning knob)
     if (conv_k1_192() && a.w3 == nullptr && a.M % 192 == 0 && a.M % 128 == 0) {
