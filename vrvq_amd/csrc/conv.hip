@@ -532,7 +532,7 @@ static int conv_ph128() {
 static int conv_k1x3_192() {
   static const int v = [] {
     const char* e = getenv("VRVQ_CONV_K1X3_192");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -613,8 +613,9 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   }
   if constexpr (KS == 1) {
     // x3 k1 GEMMs with M a multiple of 192 on 192 x 64 single-buffered tiles (154 VGPRs, three
-    // workgroups per CU; each x column block read 2x / 4x instead of 3x / 6x): tuning override
-    // VRVQ_CONV_K1X3_192=1 | 0 (default)
+    // workgroups per CU; each x column block read 2x / 4x instead of 3x / 6x): 384 x 384 at
+    // T = 5568 602 -> 541 us, 768 x 768 at T = 696 253 -> 249 (profiles/r04x_k1_192_ab.txt).
+    // Tuning override VRVQ_CONV_K1X3_192=0 (128-row tiles) | 1 (default)
     if (conv_k1x3_192() && a.w3 != nullptr && a.M % 192 == 0)
       return launch_cfg<192, 64, 2, 4, KS>(a, batch, st);
     // k = 1 GEMMs with M a multiple of 192 (the 384 / 768-channel ResidualUnit k1 + skip):
