@@ -209,7 +209,11 @@ class ResidualUnit(nn.Module):
         For C in ops.RU_FUSED_CHANNELS one launch (vrvq_residual_unit: block[2](h) stays in
         LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
         k1 conv adds the skip. Either way the output is (y if want_raw, out_snake(y)) (bit for
-        bit the same for C <= 192, include/vrvq.h)."""
+        bit the same where both forms run the k7 with the same K chunking; the two-launch k7 on
+        the 64 x 256 pair tiles -- M >= 128, T >= 640 -- sums in another order). The default
+        fused set is C = 64 / 96 / 128 (and C = 256 without the x3 weights): C = 192 runs as two
+        launches since the 192-row x3 k1 tiles (+2.8 % end to end,
+        profiles/r04z_ru_fusion_ab.txt)."""
         C = x.shape[1]
         # C = 256 with the x3 weights: the two launches (k7 on the x3 path at 128-row tiles,
         # then k1 + skip) beat the fused kernel, whose 256-row x3 weight stage does not fit

@@ -130,7 +130,7 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
-RU_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("VRVQ_RU_FUSED", "64,96,128,192,256").split(",") if c)
+RU_FUSED_CHANNELS = tuple(int(c) for c in os.environ.get("VRVQ_RU_FUSED", "64,96,128,256").split(",") if c)
 
 # The bf16x3 split MFMA path (include/vrvq.h, csrc/conv_x3.h) for the stride-1 convs of the
 # inference path; VRVQ_CONV_X3=0 keeps every conv on the fp32-input MFMA (A/B and tests).
