@@ -537,16 +537,6 @@ static int conv_k1x3_192() {
   return v;
 }
 
-// tuning override: VRVQ_CONV_PAIR_M64=1 lets the 64 x 256 pair k7 tile take M = 64 (the
-// C = 64 k7 layers when their ResidualUnits run as two launches) | 0 (default: M >= 128)
-static int conv_pair_m64() {
-  static const int v = [] {
-    const char* e = getenv("VRVQ_CONV_PAIR_M64");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
@@ -579,8 +569,7 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   if (a.M <= 32) return launch_cfg<32, 128, 1, 4, KS>(a, batch, st);
   if constexpr (KS == 7) {
     const int wide = conv_x3_wide();
-    if (a.w3 != nullptr && a.stride == 1 && a.up == 0 && a.M >= (conv_pair_m64() ? 64 : 128) &&
-        a.M % 64 == 0 &&
+    if (a.w3 != nullptr && a.stride == 1 && a.up == 0 && a.M >= 128 && a.M % 64 == 0 &&
         a.cin % 16 == 0 && ((wide >= 1 && a.ng >= 4096) || (wide == 2 && a.ng >= 640))) {
       return launch_cfg<64, 256, 1, 4, KS>(a, batch, st);
     }
