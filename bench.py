@@ -479,9 +479,9 @@ def main(argv=None):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "RVQ path: one torch.ops.vrvq.rvq_encode = rvq_fused_kernel, "
-                                   "one launch per <= 32 clips at T <= 96 (chain parts that "
-                                   "project their own frames -> chain -> expansion workgroups "
-                                   "fed by in-launch hand-offs)",
+                                   "one launch per <= 32 clips at T <= 96 (projection units "
+                                   "-> chain parts -> expansion workgroups, in-launch tagged-"
+                                   "granule hand-offs)",
                          "bytes_per_call": byt,
                          "kernel_us": round(kern_ms * 1e3, 2) if kern_n else None,
                          "kernel_launches_timed": kern_n,
