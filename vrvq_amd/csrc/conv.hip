@@ -518,13 +518,15 @@ static int conv_x3_wide() {
   return v;
 }
 
-// 2-tap GEMMs at T < 4096 that the padding rule sends to 64-wide tiles: tuning override
-// VRVQ_CONV_PH128=1 (the strided encoder convs through the phase-split view on 128-wide pair
-// tiles: half the weight re-streaming) | 2 (also the ConvTranspose layers) | 0 (default)
+// 2-tap GEMMs at T < 4096 that the padding rule sends to 64-wide tiles run 128-wide pair tiles
+// (half the weight re-streaming, 32-channel K chunks): 256 -> 512 s8 at T = 696 940 -> 878 us,
+// ConvT 768 -> 384 s8 1388 -> 1296 us (profiles/r04ze_ph128_ab.txt). Tuning override
+// VRVQ_CONV_PH128=1 (the strided encoder convs only) | 0 (64-wide) | 2 (default: also the
+// ConvTranspose layers)
 static int conv_ph128() {
   static const int v = [] {
     const char* e = getenv("VRVQ_CONV_PH128");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
