@@ -107,6 +107,15 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
+/* vrvq_conv1d (stride 1, no residual / epilogue / output Snake) writing y FRAME-MAJOR:
+ * y_fm[b][t][co] (tout x cout per clip, cout % 4 == 0, 16-byte aligned) -- the encoder's last
+ * conv (models/dac_vrvq.py:34) producing z in the layout of vrvq_rvq_encode_fm's zt, straight
+ * from the MFMA accumulators (no transpose pass). Same values as vrvq_conv1d's y. */
+int vrvq_conv1d_fm(const float* x, int batch, int cin, int tin, const float* alpha,
+                   const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
+                   int cout_pad, int k, int pad, int dil, const float* bias, float* y_fm,
+                   int tout, vrvq_stream_t stream);
+
 /* fp32 convolution on the bf16 matrix cores (the "x3" path, vrvq_amd/csrc/conv_x3.h): with
  * w_x3 = vrvq_pack_x3_weight(w_packed) (null: the fp32-input MFMA path) the stride-1 convs
  * (k in {1, 2, 3, 7}; also the ConvTranspose1d and the ResidualUnit's k7) split both operands
@@ -239,12 +248,20 @@ int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
  * path (1 or 2), or VRVQ_ERR_ARG. */
 int vrvq_rvq_path(int path);
 
-/* The fused launch's in-kernel waits are bounded: a wait that runs out (a hang averted: it
- * cannot happen with the whole grid resident) records a code in the stream's sync block and the
- * launch runs on with garbage. *code = that code (1: a chain part's wait for the projection
- * partials, 2: an expansion wait for a stage) or 0, and it is cleared. Synchronises the
- * stream. */
+/* The fused launches' in-kernel waits are bounded. A wait that runs out (a hang averted: it
+ * cannot happen with the whole grid resident) records a code in the stream's sync block and in
+ * a host-mapped word of the process, and the workgroup POISONS its outputs (codes -1, latents /
+ * z_q / z_q_is NaN) instead of passing garbage off as results. Codes: 1 a chain part's wait for
+ * the projection partials, 2 an expansion wait for a stage.
+ * vrvq_rvq_sync_error: *code = the stream's word or 0, and clears it; synchronises the stream.
+ * vrvq_rvq_pending_error: *code = the process word or 0 (a timeout of any launch that has
+ * completed by now), and clears it; no synchronisation -- the torch ops call it at entry and
+ * raise RuntimeError on a nonzero code.
+ * vrvq_rvq_debug: test hook -- every later fused launch bounds its waits at spin_max polls
+ * (0: the default ~0.5 s) and delays the first chain part by stall x s_sleep(127). */
 int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code);
+int vrvq_rvq_pending_error(int* code);
+int vrvq_rvq_debug(unsigned spin_max, unsigned stall);
 
 /* Kernel timing of the fused launch (bench.py's roofline): while on (process-wide), every fused
  * launch of vrvq_rvq_encode carries a pair of HIP events in its own dispatch
@@ -254,18 +271,43 @@ int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code);
 int vrvq_rvq_timing(int on);
 int vrvq_rvq_timing_read(float* mean_ms, int* count);
 
+/* The whole quantizer from FRAME-MAJOR z: zt[b][t][c] (B x T x D; vrvq_conv1d_fm writes it).
+ * ONE launch per group of resident clips, any T: each chain part (<= 16 frames of a clip)
+ * projects its own frames (its zt rows are contiguous: no line amplification, no partial
+ * hand-off between workgroups) on the bf16 matrix cores with the exact three-term split of both
+ * operands (fp32 accuracy), runs the 8-dim chain and publishes every stage's zst rows; expansion
+ * workgroups (clip, 128 frames, 128 channels) write z_q_is / z_q under the chain. Outputs, layouts
+ * and expressions as vrvq_rvq_encode. w3in = vrvq_rvq_pack_w_in(w_in_t) (once per weight
+ * version, vrvq_rvq_w_in_planes_size uint16 elements). Hand-off granules: eager calls use a
+ * library-owned area per (device, stream) (workspace may be NULL); under stream capture pass a
+ * workspace of >= vrvq_rvq_workspace_fm bytes (zeroed by captured memsets). VRVQ_ERR_UNSUPPORTED
+ * when the shape does not fit the launch (the caller then transposes and takes
+ * vrvq_rvq_encode). Replaces models/quantize.py:353-365, 389-421 like vrvq_rvq_encode. */
+int vrvq_rvq_w_in_planes_size(int nq, int dim, int cdim, long long* n_u16);
+int vrvq_rvq_pack_w_in(const float* w_in_t, int nq, int dim, int cdim, uint16_t* w3in,
+                       vrvq_stream_t stream);
+int vrvq_rvq_workspace_fm(int batch, int frames, int nq, int ncode, long long* bytes);
+int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frames, int nq, int ncode,
+                       int cdim, const uint16_t* w3in, const float* b_in, const float* cb,
+                       const float* cbf, const float* c2, const float* w_out, const float* b_out,
+                       const float* mcol, const float* qb, const float* imp, float level,
+                       int64_t* codes, float* latents, float* loss_pf, float* z_q_is, float* z_q,
+                       float* mask, void* workspace, long long workspace_bytes,
+                       vrvq_stream_t stream);
+
 /* The whole quantizer, the replacement of VBRResidualVectorQuantize.forward's quantizer loop,
  * importance mask and masked sum (models/quantize.py:353-365, 389-421) and of
  * ResidualVectorQuantize.forward in eval (:136-214): one fused launch (projection units, chain
  * parts that publish every stage's zst rows, expansion workgroups that write z_q_is / z_q
  * under the chain; see vrvq_rvq_path) or three stream-ordered launches (project -> chain ->
  * expand, the steps below). The fused launch hands data between its workgroups as tagged 8-byte
- * granules in the workspace (the tag carries a per-call epoch, so nothing needs clearing
- * between eager calls); the launches of a stream share a small sync block (the error word) the
- * library allocates on first use (hipMalloc, outside any stream capture); under stream capture
- * memsets of it and of the granule areas are captured in front of each launch (every replay
- * uses the same epoch). workspace: >= vrvq_rvq_workspace() bytes, 16-byte aligned,
- * caller-owned, no initialisation needed. */
+ * granules (the tag carries a per-call epoch from ONE process-wide counter, so nothing needs
+ * clearing between eager calls on any stream): eager calls use a library-owned granule area
+ * per (device, stream), allocated with the stream's sync block on first use (hipMalloc, outside
+ * any stream capture); under stream capture the granules live in the workspace, and memsets of
+ * it and of the sync block are captured in front of each launch (every replay uses epoch 1).
+ * workspace: >= vrvq_rvq_workspace() bytes, 16-byte aligned, caller-owned, no initialisation
+ * needed. */
 int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, int nq, int ncode, int cdim,
                     const float* w_in_t, const float* b_in, const float* cb, const float* cbf,
                     const float* c2, const float* w_out, const float* b_out, const float* mcol,

@@ -28,8 +28,9 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
     ap.add_argument("--variants", default="3,2", help="projection kernel variants to time (1,2,3)")
-    ap.add_argument("--paths", default="2,1",
-                    help="RVQ launch structures to time (2 fused, 1 three launches)")
+    ap.add_argument("--paths", default="fm,2,1",
+                    help="RVQ launch structures to time (fm: frame-major fused launch, 2 fused, "
+                         "1 three launches)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -42,11 +43,26 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
                                  want_z_q_is=not args.no_zqis)
+    zt = z.transpose(1, 2).contiguous()
+    w3in = st.w3in()
+    run_fm = lambda: ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,  # noqa: E731
+                                       st.b_out, st.mcol, st.qb, imp=imp, level=1.0,
+                                       want_z_q_is=not args.no_zqis)
     from vrvq_amd import _lib
-    for path, v in [(int(p), int(x)) for p in args.paths.split(",")
-                    for x in args.variants.split(",")]:
-        _lib.rvq_project_variant(v)
-        _lib.rvq_path(path)
+    runs = []
+    for p in args.paths.split(","):
+        if p == "fm":
+            runs.append(("fm", 0))
+        else:
+            runs += [(int(p), int(x)) for x in args.variants.split(",")]
+    for path, v in runs:
+        if path == "fm":
+            run = run_fm
+        else:
+            run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
+                                         want_z_q_is=not args.no_zqis)
+            _lib.rvq_project_variant(v)
+            _lib.rvq_path(path)
         ts = []
         for it in range(args.iters):
             e0.record()
@@ -64,12 +80,22 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         b2b = e0.elapsed_time(e1) * 1e3 / args.iters
+        # the fused launches' own duration (HIP events in their dispatch packets)
+        _lib.rvq_timing_read()
+        _lib.rvq_timing(True)
+        for _ in range(args.iters):
+            run()
+        torch.cuda.synchronize()
+        kms, kn = _lib.rvq_timing_read()
+        _lib.rvq_timing(False)
         byt = rvq_bytes(args.batch, args.frames, args.nq)
         tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
         print(f"path {path} projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
               f"{med:.1f} us (min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "
               f"({byt / med / 1e3 / 8000:.3f} of 8 TB/s), {byt / 1e6:.1f} MB; back to back "
-              f"{b2b:.1f} us/call ({byt / b2b / 1e3 / 8000:.3f})")
+              f"{b2b:.1f} us/call ({byt / b2b / 1e3 / 8000:.3f})"
+              + (f"; kernel {kms * 1e3:.1f} us x {kn // args.iters} launches/call "
+                 f"({byt / (kms * 1e3 * (kn // args.iters)) / 1e3 / 8000:.3f})" if kn else ""))
 
 
 if __name__ == "__main__":

@@ -32,6 +32,9 @@ def main():
                     help="z_q_is not materialised (the expansion writes z_q only)")
     ap.add_argument("--no-expand-mfma", action="store_true",
                     help="timing experiment: the expansion skips its MFMAs (outputs not checked)")
+    ap.add_argument("--fm", action="store_true",
+                    help="the frame-major launch (vrvq_rvq_encode_fm: chain parts project their "
+                         "own frames)")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", "libvrvq_hip_stamps.so"))
     lib.vrvq_rvq_path.restype = ctypes.c_int
@@ -60,8 +63,21 @@ def main():
     grid = 2 * B * 8
     stamps = torch.zeros(grid * 64, dtype=torch.int64, device=dev)
 
+    zt = z.transpose(1, 2).contiguous()
+    w3in = st.w3in()
+    assert T <= 128, "the frame-major timeline assumes 8 chain parts per clip"
+
     def run(with_stamps):
         lib.vrvq_debug_set_fused_stamps(P(stamps) if with_stamps else None)
+        if args.fm:
+            rc = lib.vrvq_rvq_encode_fm(P(zt), B, 1024, T, nq, 1024, 8, P(w3in), P(st.b_in),
+                                        P(st.cb), P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
+                                        P(st.mcol), P(st.qb), P(imp), ctypes.c_float(1.0),
+                                        P(codes), P(lat), P(loss),
+                                        None if args.no_zqis else P(zqis), P(zq), P(mask), None,
+                                        ctypes.c_longlong(0), stream)
+            assert rc == 0, rc
+            return
         rc = lib.vrvq_rvq_encode(P(z), B, 1024, T, nq, 1024, 8, P(st.w_in_t), P(st.b_in),
                                  P(st.cb), P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
                                  P(st.mcol), P(st.qb), P(imp), ctypes.c_float(1.0), P(codes),
@@ -83,7 +99,11 @@ def main():
         torch.cuda.synchronize()
         lib.vrvq_debug_set_fused_flags(0)
         print("expansion MFMAs skipped (timing experiment)")
-    ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
+    if args.fm:
+        ref = vrvq_amd.ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
+                                         st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
+    else:
+        ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
     assert torch.equal(ref[0], codes), "stamped build disagrees with the product library"
     if args.no_expand_mfma:
         zq.copy_(ref[4])
@@ -102,9 +122,12 @@ def main():
     print(f"B={B} nq={nq} T={T}: {B * 8} projection/chain + {B * 8} expansion workgroups (us)")
     print("projection / chain workgroups")
     row("start", pc[:, 0])
-    row("z slab in LDS", pc[:, 44])
+    row("z slab in LDS" if not args.fm else "K-half 0 staged", pc[:, 44])
+    if args.fm:
+        row("K-half 1 staged", pc[:, 46])
     row("projection MFMAs + stores issued", pc[:, 45])
-    row("clip's partials seen (thread 0)", pc[:, 2])
+    if not args.fm:
+        row("clip's partials seen (thread 0)", pc[:, 2])
     row("prologue done", pc[:, 3])
     for i in range(nq):
         row(f"stage {i} end", pc[:, 4 + i])

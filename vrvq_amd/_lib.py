@@ -26,6 +26,7 @@ SIGNATURES = {
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
+    "vrvq_conv1d_fm": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
     "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
@@ -40,6 +41,11 @@ SIGNATURES = {
     "vrvq_rvq_workspace": [_I, _I, _I, _P],
     "vrvq_rvq_encode": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
                         _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
+    "vrvq_rvq_w_in_planes_size": [_I, _I, _I, _P],
+    "vrvq_rvq_pack_w_in": [_P, _I, _I, _I, _P, _P],
+    "vrvq_rvq_workspace_fm": [_I, _I, _I, _I, _P],
+    "vrvq_rvq_encode_fm": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                           _F, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_rvq_project": [_P, _I, _I, _I, _I, _I, _P, _P, _P],
     "vrvq_rvq_chain": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P,
                        _P],
@@ -76,7 +82,8 @@ SIGNATURES = {
 EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I),
          "vrvq_rvq_project_variant": ([_I], _I), "vrvq_rvq_path": ([_I], _I),
          "vrvq_rvq_sync_error": ([_P, _P], _I), "vrvq_rvq_timing": ([_I], _I),
-         "vrvq_rvq_timing_read": ([_P, _P], _I)}
+         "vrvq_rvq_timing_read": ([_P, _P], _I), "vrvq_rvq_pending_error": ([_P], _I),
+         "vrvq_rvq_debug": ([ctypes.c_uint, ctypes.c_uint], _I)}
 
 _lock = threading.Lock()
 _lib = None
@@ -130,6 +137,20 @@ def rvq_sync_error(stream: int) -> int:
     code = ctypes.c_int(0)
     call("vrvq_rvq_sync_error", ctypes.c_void_p(stream), ctypes.byref(code))
     return code.value
+
+
+def rvq_pending_error() -> int:
+    """Timeout code of any fused RVQ launch completed by now (0: none), no synchronisation;
+    clears it."""
+    code = ctypes.c_int(0)
+    call("vrvq_rvq_pending_error", ctypes.byref(code))
+    return code.value
+
+
+def rvq_debug(spin_max: int = 0, stall: int = 0) -> None:
+    """Test hook: bound every later fused launch's waits at spin_max polls (0: default) and delay
+    its first chain part by stall x s_sleep(127)."""
+    call("vrvq_rvq_debug", ctypes.c_uint(spin_max), ctypes.c_uint(stall))
 
 
 def rvq_timing(on: bool) -> bool:

@@ -624,6 +624,17 @@ struct ChainLds {
 // The sync block holds only the error word of the bounded waits.
 constexpr unsigned SPIN_MAX = 1u << 19;  // bounded spins (~0.5 s); on the bound: *err = code
 
+// A bounded wait that ran out (a hang averted: it cannot happen with the whole grid resident)
+// records its code in the stream's sync block (vrvq_rvq_sync_error) and in the process's
+// host-mapped error word (system scope: the host reads it without synchronising, and the next
+// vrvq_rvq_encode* call / torch op raises on it: vrvq_rvq_pending_error). The workgroup then
+// poisons its outputs (codes -1, z_q / z_q_is NaN) instead of publishing garbage as valid data.
+__device__ __forceinline__ void report_timeout(unsigned* err, unsigned* err_host, unsigned code) {
+  __hip_atomic_store((gu32*)err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (err_host)
+    __hip_atomic_store((gu32*)err_host, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
   return __hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -632,27 +643,10 @@ __device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
   __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave: lanes < n poll flags[lane] until every one is >= target. Returns the smallest word
-// seen (>= target), or 0 after SPIN_MAX polls (then *err = code).
-__device__ __forceinline__ unsigned wave_wait_ge(const unsigned* flags, int n, unsigned target,
-                                                 unsigned* err, unsigned code) {
-  const int lane = threadIdx.x & 63;
-  const unsigned* p = flags + (lane < n ? lane : 0);
-  for (unsigned it = 0; it < SPIN_MAX; ++it) {
-    const unsigned v = ld_flag(p);
-    if (__builtin_amdgcn_ballot_w64(lane < n && v < target) == 0) {
-      unsigned mn = 0xffffffffu;
-      for (int l = 0; l < n; ++l) mn = min(mn, (unsigned)__builtin_amdgcn_readlane((int)v, l));
-      return mn;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (lane == 0) st_flag(err, code);
-  return 0;
-}
-
-struct ChainHandoff {              // fused launch only
+struct ChainHandoff {              // fused launches only
   unsigned* err;
+  unsigned* err_host;              // host-mapped error word (report_timeout) or null
+  unsigned spin_max;               // bound of every wait (SPIN_MAX; smaller in the timeout test)
   unsigned epoch;
   __amdgpu_buffer_rsrc_t part;     // the partials' tagged granules, read with sc1 loads
   unsigned long long* zsh;         // this part's stage-0 block of tagged zst granules
@@ -660,9 +654,15 @@ struct ChainHandoff {              // fused launch only
   unsigned long long* stamps;      // diagnostic build only
 };
 
-template <int NM, bool FUSED>
+// Where a chain part gets pu = (P + b_in) - Qb of its frames: CH_SPLIT the 8 split partials of
+// the three-launch path (plain loads after the projection kernel), CH_GRANULE the tagged
+// partial granules of rvq_fused_kernel, CH_LOCAL already in LDS (rvq_fm_kernel's own projection).
+constexpr int CH_SPLIT = 0, CH_GRANULE = 1, CH_LOCAL = 2;
+
+template <int NM, int MODE>
 __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0, int nf,
                                            const ChainHandoff& hx) {
+  constexpr bool FUSED = MODE != CH_SPLIT;  // in-launch hand-offs: publishes every stage's zst
   constexpr int N = 256 * NM;
   constexpr int NPW = N / CH_NW;   // codes per wave
   constexpr int NT = NPW / 16;     // 16-code MFMA tiles per wave
@@ -709,7 +709,11 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
     for (int e = tid; e < R * RCD / 4; e += CH_NT)
       reinterpret_cast<float4*>(m_s)[e] = ld4(a.mcol + (size_t)e * 4);
   // ---- prologue: pu = (P + b_in) - Qb (partials summed in split order); stage 0 operands.
-  if constexpr (FUSED) {
+  __shared__ int dead_s;  // a bounded wait ran out in this workgroup: outputs poisoned
+  if (tid == 0) dead_s = 0;
+  if constexpr (MODE == CH_LOCAL) {
+    // pu_s filled by the caller (project_fm_body) before the barrier that precedes this call
+  } else if constexpr (MODE == CH_GRANULE) {
     // the clip's 8 partials of this part's frames: tagged granules (16-B sc1 loads, two each),
     // each thread re-reads its item until every tag is this call's (the projection units of
     // the clip run concurrently on other CUs); R = 8 nq: the frames' rows are contiguous
@@ -729,8 +733,9 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
           ok = ok && v[sp][0][1] == ptag && v[sp][0][3] == ptag && v[sp][1][1] == ptag &&
                v[sp][1][3] == ptag;
         if (ok) break;
-        if (it == SPIN_MAX) {
-          st_flag(hx.err, 1u);
+        if (it >= hx.spin_max) {
+          report_timeout(hx.err, hx.err_host, 1u);
+          dead_s = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(4);
@@ -984,20 +989,22 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
   }
   CSTAMP(nq, 2);
 
-  // ---- epilogue: outputs of every stage (LDS -> HBM)
+  // ---- epilogue: outputs of every stage (LDS -> HBM); poisoned after a timed-out wait
+  const bool dead = FUSED && dead_s != 0;
   for (int e = tid; e < nf * nq * RCD; e += CH_NT) {
     // zst [b][i][t][k] and latents [b][i*8+k][t]
     const int k = e & 7, fi = e >> 3;
     const int i = fi / nf, f = fi - i * nf;
     const int n = n0 + f, b = n / a.T, t = n - b * a.T;
     if (a.zst) a.zst[(((size_t)b * nq + i) * a.T + t) * RCD + k] = zs_s[(f * nq + i) * RCD + k];
-    a.latents[(((size_t)b * nq + i) * RCD + k) * a.T + t] = lat_s[(f * nq + i) * RCD + k];
+    a.latents[(((size_t)b * nq + i) * RCD + k) * a.T + t] =
+        dead ? __builtin_nanf("") : lat_s[(f * nq + i) * RCD + k];
   }
   for (int e = tid; e < nf * nq; e += CH_NT) {
     const int i = e / nf, f = e - i * nf;
     const int n = n0 + f, b = n / a.T, t = n - b * a.T;
     const size_t o = ((size_t)b * nq + i) * a.T + t;
-    a.codes[o] = (int64_t)code_s[f * nq + i];
+    a.codes[o] = dead ? (int64_t)-1 : (int64_t)code_s[f * nq + i];
     a.loss_pf[o] = loss_s[f * nq + i];
     if (a.mask) {
       const float s = a.imp ? (a.imp[n] * a.level) * (float)nq : INFINITY;
@@ -1012,17 +1019,18 @@ template <int NM>
 __global__ __launch_bounds__(CH_NT) void rvq_chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n0 = blockIdx.x * a.F;
-  chain_body<NM, false>(a, sm, n0, min(a.F, a.NF - n0), ChainHandoff{});
+  chain_body<NM, CH_SPLIT>(a, sm, n0, min(a.F, a.NF - n0), ChainHandoff{});
 }
 
 // ------------------------------------------------------------------------------------------
 // Expansion on the matrix cores: z_q_is[b,i,c,t] = (W_out(i)[c,:] . zst[b,i,t,:]) + b_out(i)[c]
 // and z_q[b,c,t] = sum_i mask[b,i,t] * z_q_is[b,i,c,t] (stage order, from 0: the masked_sum
 // kernel's expression bit for bit). One wave = one (clip, 32-channel, 32-frame) tile over all
-// stages; per stage five v_mfma_f32_32x32x2_f32 with K = 10: k < 8 the out_proj weights x zst,
-// k = 8 the bias x 1, k = 9 zero -- the k-ordered fma chain from 0, i.e. dot8(W, zst) + bias
-// with the reference's roundings. The accumulator layout puts 32 consecutive frames of one
-// channel row in each half-wave, so every store instruction writes two 128-B row runs.
+// stages; per stage four v_mfma_f32_32x32x2_f32 (K = 8: the out_proj weights x zst, the
+// k-ordered fma chain from 0) and the bias as one VALU add -- dot8(W, zst) + bias with the
+// reference's roundings (r05: the bias was a 9th k of a fifth MFMA, the same value up to the
+// sign of an exact zero). The accumulator layout puts 32 consecutive frames of one channel row
+// in each half-wave, so every store instruction writes two 128-B row runs.
 struct ExpandArgs {
   const float* zst;    // [B][nq][T][8]
   int B, D, T, nq;
@@ -1064,17 +1072,23 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
   for (int r = 0; r < 16; ++r) zq[r] = 0.0f;
   // operands of stage i, software-pipelined one stage ahead (the wait for them never covers
   // the previous stage's stores: vmcnt counts stores too)
+  // b_out of the accumulator rows c0 + 4 h + (r & 3) + 8 (r >> 2) (clamped at a D % 32 tail:
+  // those rows are not stored; D >= 4), loaded for the current stage ahead of the next stage's
+  // prefetch
   float4 w0 = ld4(wp), w1 = ld4(wp + 4), z0 = ld4(zp), z1 = ld4(zp + 4);
-  float bb = a.b_out[cr];
   for (int i = 0; i < a.nq; ++i) {
     const float4 cw0 = w0, cw1 = w1, cz0 = z0, cz1 = z1;
-    const float cb = bb;
+    float cb[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = ld4(a.b_out + (size_t)i * a.D + min(c0 + 4 * h + 8 * q, a.D - 4));
+      cb[4 * q] = v.x; cb[4 * q + 1] = v.y; cb[4 * q + 2] = v.z; cb[4 * q + 3] = v.w;
+    }
     if (i + 1 < a.nq) {
       w0 = ld4(wp + (i + 1) * wstride);
       w1 = ld4(wp + (i + 1) * wstride + 4);
       z0 = ld4(zp + (i + 1) * zstride);
       z1 = ld4(zp + (i + 1) * zstride + 4);
-      bb = a.b_out[(size_t)(i + 1) * a.D + cr];
     }
     // lane (col, h) supplies k = 2 s + h of step s
     const float wa[4] = {h ? cw0.y : cw0.x, h ? cw0.w : cw0.z, h ? cw1.y : cw1.x, h ? cw1.w : cw1.z};
@@ -1084,8 +1098,8 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
     for (int r = 0; r < 16; ++r) q[r] = 0.0f;
 #pragma unroll
     for (int st = 0; st < 4; ++st) q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
-    // k = 8: bias x 1 (lanes h = 0), k = 9: 0 x 0 (lanes h = 1)
-    q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cb, h ? 0.0f : 1.0f, q, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) q[r] = q[r] + cb[r];
     const float m = a.mask_in ? (tv ? a.mask_in[((size_t)b * a.nq + i) * a.T + t] : 0.0f)
                               : ((s - (float)i >= 0.0f) ? 1.0f : 0.0f);  // models/utils.py:45-61
     if (a.mask && ct == 0 && h == 0 && tv) a.mask[((size_t)b * a.nq + i) * a.T + t] = m;
@@ -1111,62 +1125,86 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// The fused RVQ launch (one kernel instead of projection -> chain -> expansion; T <= 96 frames
-// per clip, every workgroup of the grid resident at once). Workgroups [0, 8 B) are (clip b,
-// split / part s): the projection unit (b, s) (project3_body, partials stored as tagged
-// granules), then chain part s of clip b (frames [s F, s F + F), F = ceil(T / 8)), which reads
-// the clip's 8 partials of its frames as they land and publishes every stage's zst. Workgroups
-// [8 B, 16 B) are the expansion: (clip b, 128-channel block) over all stages, each stage once its
-// 8 chain parts have published it, so the z_q_is write stream runs under the chain instead of
-// after it. Same values as the three launches, bit for bit (tests/test_gpu_parity.py).
-constexpr int FU_NP = PJ_SPLIT;     // chain parts per clip
-constexpr int FU_ROWS = 16;         // frames per part block of the stage hand-off rows
+// The fused RVQ launches: one kernel instead of projection -> chain -> expansion, every
+// workgroup of the grid resident at once (clips per launch from the occupancy query).
+//
+// rvq_fused_kernel (z [B][D][T], T <= 96): workgroups [0, 8 B) are (clip b, split / part s): the
+// projection unit (b, s) (project3_body, partials stored as tagged granules), then chain part s
+// of clip b (frames [s F, s F + F), F = ceil(T / 8)), which reads the clip's 8 partials of its
+// frames as they land and publishes every stage's zst.
+//
+// rvq_fm_kernel (frame-major zt [B][T][D], any T): workgroups [0, B P) are chain parts (clip b,
+// frames [p F, p F + F), F <= 16) that project their own frames (project_fm_body: the part's zt
+// rows are contiguous, no partial leaves the workgroup) and run the chain.
+//
+// In both, the workgroups after the chain parts are the expansion: (clip b, 128-frame block fb,
+// 128-channel block cb) over all stages, each stage once the chain parts of its frames have
+// published it, so the z_q_is write stream runs under the chain instead of after it. Same
+// expressions as the three launches (tests/test_gpu_parity.py).
+constexpr int FU_NP = PJ_SPLIT;     // chain parts per clip of rvq_fused_kernel
+constexpr int FU_ROWS = 16;         // frames per part block of the stage hand-off rows (F <= 16)
 constexpr int FU_CB = 128;          // channels per expansion workgroup
-constexpr int SYNC_ERR = 2048;      //                   first timeout code (1 projection, 2 stage)
+constexpr int FU_FB = 128;          // frames per expansion workgroup
+constexpr int SYNC_ERR = 2048;      // the error word (1 partials wait, 2 stage wait)
 constexpr int SYNC_WORDS = 2052;    // used words (x 4 = 8208 B, a multiple of 16)
-constexpr int FU_CLIPS_MAX = 32;    // clips per launch (flag slots)
+constexpr int FU_CLIPS_MAX = 32;    // clips per rvq_fused_kernel launch
 
 struct FusedArgs {
   ChainArgs c;                      // part (workspace), B, T, nq, F, NF; outputs
-  const float* z;                   // [B][D][T]
+  const float* z;                   // [B][D][T] (rvq_fused_kernel) or zt [B][T][D] (rvq_fm_kernel)
   const float* w_in_t;
+  const u32x4* w3in;                // rvq_fm_kernel: W_in planes (vrvq_rvq_pack_w_in)
   const float* w_out;               // [nq][D][8]
   const float* b_out;               // [nq][D]
   float* z_q_is;                    // [B][nq][D][T] or null
   float* z_q;                       // [B][D][T]
-  unsigned long long* zsh;          // [B][nq][FU_NP][FU_ROWS][8] tagged zst granules
+  unsigned long long* zsh;          // [B][nq][P][FU_ROWS][8] tagged zst granules
   int zsh_bytes;
+  int P;                            // chain parts per clip
+  int n_fb;                         // expansion frame blocks per clip
   unsigned* sync;
+  unsigned* err_host;               // host-mapped error word (report_timeout) or null
+  unsigned spin_max;
+  unsigned stall;                   // test knob: chain part 0's start delayed by stall x s_sleep(127)
   unsigned epoch;
   unsigned long long* stamps;       // diagnostic build only
   int dbg;                          // diagnostic build only: bit 0 = expansion skips its MFMAs
 };
 
-// Expansion workgroup (clip b, channels [128 cb, +128)): wave w = 32-channel tile (w & 3) x
-// 32-frame tiles {w >> 2, (w >> 2) + 2}; per stage five v_mfma_f32_32x32x2_f32 per tile exactly
-// as rvq_expand_kernel (K = 10: W_out x zst, bias x 1). Every wave runs on its own (no barrier).
+// Expansion workgroup (clip b, frames [128 fb, +128), channels [128 cb, +128)): wave w =
+// 32-channel tile (w & 3) x 32-frame tiles {w >> 2, (w >> 2) + 2} of the block; per stage four
+// v_mfma_f32_32x32x2_f32 per tile (K = 8: W_out x zst, the k-ordered fma chain) and the bias as
+// one VALU add -- rvq_expand_kernel's expression (dot8(W, zst) + bias) with one matrix-core op
+// fewer per tile and stage than the bias-as-9th-k form. Every wave runs on its own (no barrier).
 // The stage's zst rows are tagged granules (the chain's S2 stores): a wave loads stage i + 1's
 // granules (and W_out / b_out rows) speculatively BEFORE stage i's z_q_is stores and checks
 // their tags when it gets there -- vmcnt retires in order, so a load issued after the stores
 // would wait for them to drain (with flag words trailing the data the workgroup ran ~4 us per
 // stage, bound by its own store queue: profiles/r04d_fused_timeline.txt). Rows whose tags are
-// not this call's stage yet are re-read until they are (bounded).
+// not this call's stage yet are re-read until they are (bounded; on the bound the tile's
+// outputs are NaN).
 struct ExOps {
   float4 w0, w1;
-  float bb;
   u32x4 z[2][2];  // per frame tile: 4 granules {zst k = 2 s + h, tag}, s = 0..3
 };
 
-__device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
+// sm: the launch's LDS (unused by the expansion role otherwise): b_out of the workgroup's 128
+// channels for every stage, so a lane reads the bias of its 16 accumulator rows as four
+// broadcast ds_read_b128 per stage instead of keeping them in registers a stage ahead.
+__device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, float* sm) {
   const int nq = f.c.nq, T = f.c.T, F = f.c.F;
-  const int b = e / (RD / FU_CB), cb = e - b * (RD / FU_CB);
+  constexpr int NCB = RD / FU_CB;
+  const int cb = e % NCB;
+  const int fb = (e / NCB) % f.n_fb;
+  const int b = e / (NCB * f.n_fb);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = cb * FU_CB + (wave & 3) * 32;
   const int col = lane & 31, h = lane >> 5;
-  const int n_ft = (T + 31) / 32;
+  const int n_ft = (min(FU_FB, T - fb * FU_FB) + 31) / 32;  // frame tiles of this block
   const int ft0 = wave >> 2;
-  const bool two = ft0 + 2 < n_ft;  // wave-uniform
+  const bool one = ft0 < n_ft;       // wave-uniform: the wave has a first tile
+  const bool two = ft0 + 2 < n_ft;   // ... and a second
   const __amdgpu_buffer_rsrc_t zr =
       __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
   int zoff[2];  // byte offset of this lane's 4 granules of stage 0
@@ -1175,15 +1213,15 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
   float sc[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int t = (ft0 + 2 * j) * 32 + col;
+    const int t = fb * FU_FB + (ft0 + 2 * j) * 32 + col;
     tt[j] = t;
-    tv[j] = t < T && (j == 0 || two);
+    tv[j] = t < T && (j == 0 ? one : two);
     const int tc = min(t, T - 1);
     const int p = tc / F, fr = tc - p * F;
-    zoff[j] = (((b * nq * FU_NP + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
+    zoff[j] = ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
     sc[j] = (f.c.imp && tv[j]) ? (f.c.imp[(size_t)b * T + tc] * f.c.level) * (float)nq : INFINITY;
   }
-  const int zstage = FU_NP * FU_ROWS * RCD * 8;  // bytes per stage
+  const int zstage = f.P * FU_ROWS * RCD * 8;  // bytes per stage
   const int cr = c0 + col;  // A-operand row of this lane
   const float* wp = f.w_out + (size_t)cr * RCD;
   const size_t wstride = (size_t)RD * RCD;
@@ -1199,7 +1237,6 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
   auto load = [&](int i, ExOps& o) {
     o.w0 = ld4(wp + i * wstride);
     o.w1 = ld4(wp + i * wstride + 4);
-    o.bb = f.b_out[(size_t)i * RD + cr];
     load_z(i, o.z);
   };
   auto tagged = [&](const u32x4 (&z)[2][2], int i) -> bool {  // wave-uniform
@@ -1207,7 +1244,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
     bool good = true;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if (j == 0 || two)
+      if (j == 0 ? one : two)
         good = good && z[j][0][1] == tag && z[j][0][3] == tag && z[j][1][1] == tag &&
                z[j][1][3] == tag;
     return __builtin_amdgcn_ballot_w64(!good) == 0;
@@ -1218,27 +1255,33 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) zq[j][r] = 0.0f;
   ExOps cur;
-  bool dead = false;  // a wait ran out: no more waits (err recorded)
-  // stage 0 lands after the projection and the chain's first stage (~10 us): wave 0 alone
-  // watches its rows with a long sleep between looks, the others wait at the barrier
+  float* bias_s = sm;  // [nq][FU_CB]
+  for (int k = threadIdx.x; k < nq * FU_CB; k += CH_NT)
+    bias_s[k] = f.b_out[(size_t)(k / FU_CB) * RD + cb * FU_CB + (k % FU_CB)];
+  __shared__ int xdead_s;  // wave 0's stage-0 wait ran out (then no wave waits any more)
+  bool dead = false;       // a wait ran out: no more waits (err recorded), outputs NaN
+  // stage 0 lands after the chain's first stage: wave 0 alone watches its rows with a long
+  // sleep between looks, the others wait at the barrier
   if (wave == 0) {
     for (unsigned it = 0;; ++it) {
       load_z(0, cur.z);
       if (tagged(cur.z, 0)) break;
-      if (it == SPIN_MAX) {
-        if (lane == 0) st_flag(f.sync + SYNC_ERR, 2u);
+      if (it >= f.spin_max) {
+        if (lane == 0) report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
         dead = true;
         break;
       }
       __builtin_amdgcn_s_sleep(16);
     }
+    if (lane == 0) xdead_s = dead ? 1 : 0;
   }
   __syncthreads();
+  dead = xdead_s != 0;
   load(0, cur);
   for (int i = 0; i < nq; ++i) {
     for (unsigned it = 0; !dead && !tagged(cur.z, i); ++it) {
-      if (it == SPIN_MAX) {
-        if (lane == 0) st_flag(f.sync + SYNC_ERR, 2u);
+      if (it >= f.spin_max) {
+        if (lane == 0) report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
         dead = true;
         break;
       }
@@ -1252,9 +1295,11 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
     load(min(i + 1, nq - 1), nxt);
     const float wa[4] = {h ? cur.w0.y : cur.w0.x, h ? cur.w0.w : cur.w0.z,
                          h ? cur.w1.y : cur.w1.x, h ? cur.w1.w : cur.w1.z};
+    // bias of the accumulator rows (c0 + 4 h + (r & 3) + 8 (r >> 2)) of this lane
+    const float* brow = bias_s + i * FU_CB + (wave & 3) * 32 + 4 * h;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (j == 1 && !two) break;
+      if (!(j == 0 ? one : two)) break;
       const float zb[4] = {__uint_as_float(cur.z[j][0][0]), __uint_as_float(cur.z[j][0][2]),
                            __uint_as_float(cur.z[j][1][0]), __uint_as_float(cur.z[j][1][2])};
       f32x16 q;
@@ -1266,10 +1311,20 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
 #pragma unroll
       for (int st = 0; st < 4; ++st)
         q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
-      q = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.0f : cur.bb, h ? 0.0f : 1.0f, q, 0, 0, 0);
 #ifdef VRVQ_STAMPS
       }
 #endif
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float4 v = *reinterpret_cast<const float4*>(brow + 8 * qq);
+        q[4 * qq] = q[4 * qq] + v.x;
+        q[4 * qq + 1] = q[4 * qq + 1] + v.y;
+        q[4 * qq + 2] = q[4 * qq + 2] + v.z;
+        q[4 * qq + 3] = q[4 * qq + 3] + v.w;
+      }
+      if (dead)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) q[r] = __builtin_nanf("");
       const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
       if (f.z_q_is && tv[j]) {
         float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
@@ -1287,9 +1342,22 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e) {
     if (tv[j]) {
       float* dst = f.z_q + ((size_t)b * RD + c0 + 4 * h) * T + tt[j];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = zq[j][r];
+      for (int r = 0; r < 16; ++r)
+        dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = dead ? __builtin_nanf("") : zq[j][r];
     }
   }
+}
+
+__device__ __forceinline__ ChainHandoff fused_handoff(const FusedArgs& f, int b, int p) {
+  ChainHandoff hx;
+  hx.err = f.sync + SYNC_ERR;
+  hx.err_host = f.err_host;
+  hx.spin_max = f.spin_max;
+  hx.epoch = f.epoch;
+  hx.zsh = f.zsh + (size_t)(b * f.c.nq * f.P + p) * FU_ROWS * RCD;
+  hx.zsh_stage = f.P * FU_ROWS * RCD;
+  hx.stamps = f.stamps;
+  return hx;
 }
 
 template <int NM, bool PJ3>
@@ -1299,7 +1367,7 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   const int blk = blockIdx.x;
   FSTAMP(f.stamps, 0);
   if (blk >= B * FU_NP) {
-    fused_expand_body(f, blk - B * FU_NP);
+    fused_expand_body(f, blk - B * FU_NP, sm);
     FSTAMP(f.stamps, 41);
     return;
   }
@@ -1310,6 +1378,8 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
       part, (short)0, (int)((size_t)PJ_SPLIT * f.c.NF * R * 8), RSRC_FLAGS);
   // projection unit (b, s): partials as tagged granules, then straight on to the chain
   PartSink out{part, pr, f.epoch * 64u};
+  if (f.stall && blk == 0)  // test knob (vrvq_rvq_debug_stall): a late producer
+    for (unsigned k = 0; k < f.stall; ++k) __builtin_amdgcn_s_sleep(127);
   if constexpr (PJ3)
     project3_body(f.z, T, nq, 0, b, s, f.w_in_t, out, f.c.NF, reinterpret_cast<char*>(sm),
                   f.stamps);
@@ -1319,14 +1389,189 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   // chain part s of clip b
   const int nf = min(F, T - s * F);
   if (nf <= 0) return;  // no frames (T < 8 F): no expansion lane reads this part's block
-  ChainHandoff hx;
-  hx.err = f.sync + SYNC_ERR;
-  hx.epoch = f.epoch;
+  ChainHandoff hx = fused_handoff(f, b, s);
   hx.part = pr;
-  hx.zsh = f.zsh + (size_t)(b * nq * FU_NP + s) * FU_ROWS * RCD;
-  hx.zsh_stage = FU_NP * FU_ROWS * RCD;
-  hx.stamps = f.stamps;
-  chain_body<NM, true>(f.c, sm, b * T + s * F, nf, hx);
+  chain_body<NM, CH_GRANULE>(f.c, sm, b * T + s * F, nf, hx);
+}
+
+// ------------------------------------------------------------------------------------------
+// Local projection of one chain part of rvq_fm_kernel: pu[f][r] = (P[f][r] + b_in[r]) - qb[r],
+// P[f][r] = sum_c W_in[r][c] zt[b][t0 + f][c], for the part's nf <= 16 frames and every row
+// r < R = 8 nq, on v_mfma_f32_16x16x32_bf16 with both operands split exactly into three bf16
+// terms and the six products of conv_x3.h (dropped terms <= 2^-23 |ab|: fp32 accuracy). The
+// part's zt rows are contiguous (4 KB each: no line amplification), staged in LDS as three bf16
+// planes one K-half (512 channels) at a time, [plane][frame][channel] with 1040-B rows
+// (conflict-free 16-B B-operand reads); W_in comes pre-split in the MFMA A-fragment order
+// (w3in [32 k-steps][3 planes][R/16 row tiles][64 lanes] x 16 B, vrvq_rvq_pack_w_in), read
+// from L2 straight into registers, four k-steps in flight. Work item = (row tile rt, K part kq)
+// with S K parts when fewer than 8 row tiles (nq = 8: 4 tiles x 2 parts over the 8 waves); the
+// S partial accumulators are summed in kq order through LDS. Frames >= nf are clamped copies
+// whose output columns are never read.
+constexpr int LP_LD = 520;                        // bf16 per frame row of a K-half plane
+constexpr int LP_PLANE = FU_ROWS * LP_LD * 2;     // bytes per plane (16 frame rows)
+constexpr int LP_LDS = 3 * LP_PLANE;              // 49,920 B
+
+__host__ __device__ inline int fm_nrt(int nq) { return (nq * RCD + 15) / 16; }
+__host__ __device__ inline int fm_ksplit(int nq) {  // K parts per row tile
+  const int n = fm_nrt(nq);
+  return n >= 8 ? 1 : n >= 4 ? 2 : n >= 2 ? 4 : 8;
+}
+// LDS of rvq_fm_kernel: the chain carve, overlaid by the K-half planes during the projection,
+// then the S - 1 partial tiles of the K split
+__host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
+  size_t c = (size_t)ChainLds(nq, F, N).total * sizeof(float);
+  if (c < (size_t)LP_LDS) c = LP_LDS;
+  const int S = fm_ksplit(nq);
+  return c + (size_t)(S - 1) * fm_nrt(nq) * 64 * 16;
+}
+
+// NKS consecutive k-steps (32 channels each) of one 16-row tile against the staged K-half:
+// the A planes come from L2 in a ring three k-steps deep (36 VGPRs in flight per lane), each
+// k-step's six products in the x3 order m m, h l, l h, h m, m h, h h.
+template <int NKS>
+__device__ __forceinline__ void fm_ksteps(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
+                                          int h, const char* lds, f32x4& acc) {
+  constexpr int DEPTH = NKS < 3 ? NKS : 3;
+  const int lane = threadIdx.x & 63, lr = lane & 15, kg = lane >> 4;
+  u32x4 a[DEPTH][3];
+  auto load_a = [&](int j, u32x4 (&dst)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) dst[p] = w3[((size_t)((ks0 + j) * 3 + p) * n_rt + rt) * 64 + lane];
+  };
+#pragma unroll
+  for (int j = 0; j < DEPTH; ++j) load_a(j, a[j]);
+#pragma unroll
+  for (int j = 0; j < NKS; ++j) {
+    const int kk = (ks0 + j - 16 * h) * 32 + 8 * kg;  // channel within the half
+    const char* bp = lds + lr * (LP_LD * 2) + kk * 2;
+    const u32x4 bh = *reinterpret_cast<const u32x4*>(bp);
+    const u32x4 bm = *reinterpret_cast<const u32x4*>(bp + LP_PLANE);
+    const u32x4 bl = *reinterpret_cast<const u32x4*>(bp + 2 * LP_PLANE);
+    const u32x4(&aj)[3] = a[j % DEPTH];
+    acc = mfma16_bf16(aj[1], bm, acc);  // m m
+    acc = mfma16_bf16(aj[0], bl, acc);  // h l
+    acc = mfma16_bf16(aj[2], bh, acc);  // l h
+    acc = mfma16_bf16(aj[0], bm, acc);  // h m
+    acc = mfma16_bf16(aj[1], bh, acc);  // m h
+    acc = mfma16_bf16(aj[0], bh, acc);  // h h
+    if (j + DEPTH < NKS) load_a(j + DEPTH, a[j % DEPTH]);  // compile-time condition
+  }
+}
+
+__device__ __forceinline__ void project_fm_body(const FusedArgs& f, int b, int t0, int nf,
+                                                int N, float* sm) {
+  const int nq = f.c.nq, R = nq * RCD, T = f.c.T;
+  const int n_rt = fm_nrt(nq), S = fm_ksplit(nq);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* lds = reinterpret_cast<char*>(sm);
+  const ChainLds L(nq, f.c.F, 256);  // only .pu is used here (independent of N)
+  float* pu_s = sm + L.pu;
+  const size_t c_bytes = [&] {  // fm_lds_bytes' carve: the partial tiles after the chain's LDS
+    size_t c = (size_t)ChainLds(nq, f.c.F, N).total * sizeof(float);
+    return c < (size_t)LP_LDS ? (size_t)LP_LDS : c;
+  }();
+  f32x4* xpart = reinterpret_cast<f32x4*>(lds + c_bytes);  // [S - 1][n_rt][64 lanes]
+  // the part's zt rows: thread (c4 = tid & 127, frame group tid >> 7) holds 4 float4 per K-half
+  // (frames (tid >> 7) + 4 u, channels 512 h + 4 c4 .. +3), all in flight at once
+  const float* zb = f.z + ((size_t)b * T + t0) * RD;
+  const int c4 = tid & 127, fg = tid >> 7;
+  float4 zv[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      zv[h][u] = ld4(zb + (size_t)min(fg + 4 * u, nf - 1) * RD + 512 * h + 4 * c4);
+  const u32x4* w3 = f.w3in;
+  const int n_items = n_rt * S;  // <= 16: at most two rounds of 8 items (S = 1 at nq > 14)
+  // items of this wave: it = wave, wave + 8 (rt = it / S, kq = it % S); the summed tiles stay in
+  // registers until every wave is done with the planes (pu_s shares their LDS)
+  f32x4 res[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    const int it0 = round * CH_NW;
+    if (it0 >= n_items) break;
+    const int it = it0 + wave;
+    const bool act = it < n_items;  // wave-uniform
+    const int rt = min(it, n_items - 1) / S, kq = min(it, n_items - 1) % S;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < 2; ++h) {
+      // stage K-half h (every item round: nq >= 16 runs more than one round)
+      __syncthreads();  // the previous half's planes are no longer read
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        // select, not zv[h][u]: a runtime index sends the array to scratch
+        const float4 v = h ? zv[1][u] : zv[0][u];
+        unsigned hh[2], mm[2], ll[2];
+        rvq_split3x2(v.x, v.y, hh[0], mm[0], ll[0]);
+        rvq_split3x2(v.z, v.w, hh[1], mm[1], ll[1]);
+        char* d = lds + (fg + 4 * u) * (LP_LD * 2) + c4 * 8;
+        *reinterpret_cast<uint2*>(d) = make_uint2(hh[0], hh[1]);
+        *reinterpret_cast<uint2*>(d + LP_PLANE) = make_uint2(mm[0], mm[1]);
+        *reinterpret_cast<uint2*>(d + 2 * LP_PLANE) = make_uint2(ll[0], ll[1]);
+      }
+      __syncthreads();
+      if (round == 0) FSTAMP(f.stamps, h == 0 ? 44 : 46);  // K-half h staged
+      if (act) {
+        // this item's k-steps of half h: ks = 16 h + kq * NKS + j, j < NKS = 16 / S
+        const int ks0 = 16 * h + kq * (16 / S);
+        switch (S) {
+          case 1: fm_ksteps<16>(w3, n_rt, rt, ks0, h, lds, acc); break;
+          case 2: fm_ksteps<8>(w3, n_rt, rt, ks0, h, lds, acc); break;
+          case 4: fm_ksteps<4>(w3, n_rt, rt, ks0, h, lds, acc); break;
+          default: fm_ksteps<2>(w3, n_rt, rt, ks0, h, lds, acc); break;
+        }
+      }
+    }
+    // D layout: lane l, reg q -> row 16 rt + 4 (l >> 4) + q, frame l & 15
+    if (S > 1) {
+      if (act && kq > 0) xpart[((kq - 1) * n_rt + rt) * 64 + lane] = acc;
+      __syncthreads();
+    }
+    if (act && kq == 0) {
+      for (int q = 1; q < S; ++q) acc = acc + xpart[((q - 1) * n_rt + rt) * 64 + lane];
+      res[round] = acc;
+    }
+    if (S > 1) __syncthreads();  // xpart free for the next round
+  }
+  __syncthreads();  // every wave is done with the planes: pu_s may overwrite them
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    const int it = round * CH_NW + wave;
+    if (it >= n_items || it % S != 0) continue;
+    const int rt = it / S;
+    const int fr = lane & 15, rr = rt * 16 + 4 * (lane >> 4);
+    if (fr < nf && rr < R) {
+      const f32x4 acc = res[round];
+      float4 o;
+      o.x = (acc[0] + f.c.b_in[rr]) - f.c.qb[rr];
+      o.y = (acc[1] + f.c.b_in[rr + 1]) - f.c.qb[rr + 1];
+      o.z = (acc[2] + f.c.b_in[rr + 2]) - f.c.qb[rr + 2];
+      o.w = (acc[3] + f.c.b_in[rr + 3]) - f.c.qb[rr + 3];
+      *reinterpret_cast<float4*>(pu_s + fr * R + rr) = o;
+    }
+  }
+  __syncthreads();  // pu_s complete; the planes' LDS is the chain's from here
+}
+
+template <int NM>
+__global__ __launch_bounds__(CH_NT, 4) void rvq_fm_kernel(FusedArgs f) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = f.c.B, T = f.c.T, F = f.c.F;
+  const int blk = blockIdx.x;
+  FSTAMP(f.stamps, 0);
+  if (blk >= B * f.P) {
+    fused_expand_body(f, blk - B * f.P, sm);
+    FSTAMP(f.stamps, 41);
+    return;
+  }
+  const int b = blk / f.P, p = blk - b * f.P;
+  const int t0 = p * F, nf = min(F, T - t0);
+  if (f.stall && blk == 0)  // test knob (vrvq_rvq_debug_stall): a late producer
+    for (unsigned k = 0; k < f.stall; ++k) __builtin_amdgcn_s_sleep(127);
+  project_fm_body(f, b, t0, nf, 256 * NM, sm);
+  FSTAMP(f.stamps, 45);
+  chain_body<NM, CH_LOCAL>(f.c, sm, b * T + t0, nf, fused_handoff(f, b, p));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1455,68 +1700,132 @@ int rvq_path() {
   return g_rvq_path;
 }
 
-// Per (device, stream): the flag block the fused launches on that stream share (serialised by
-// the stream) and the last epoch used. Eager calls take epochs 2, 3, ...: every flag an older
-// call left is below this call's targets. Under stream capture the graph gets a memset node of
-// the block before the kernel and epoch 1, so every replay starts from zeros.
-struct SyncBlock {
-  unsigned* dev = nullptr;
-  unsigned epoch = 1;
+// Process-wide state of the fused launches' in-launch hand-offs:
+//  * epochs: ONE counter for every call of the process (every stream and device), so tags are
+//    unique across streams -- granules a call on another stream left can never match. At
+//    EPOCH_RESET the counter restarts at 2 and every library-owned granule area is cleared (on
+//    its own stream, ordered after the calls that used it) before a tag can repeat.
+//  * granule areas: eager calls hand off through a library-owned area per (device, stream)
+//    (hipMalloc, zeroed at allocation, grown on demand), never shared with the caller or the
+//    caching allocator: every tag word in it was written by this library (an older epoch). A
+//    caller workspace whose previous contents happened to hold 64 * epoch in a tag slot (small
+//    integer data does) could otherwise pass a check before the real granule lands.
+//  * under stream capture there is no allocation: the call uses the caller's workspace,
+//    zeroed by captured memset nodes, and epoch 1 (eager epochs start at 2); the sync block of
+//    the stream must exist from an earlier eager call, else the call takes the three launches.
+//  * the error word: a per-stream device word (vrvq_rvq_sync_error, synchronising) and one
+//    host-mapped word of the process (vrvq_rvq_pending_error, no synchronisation; the torch
+//    ops raise on it at their next call).
+struct StreamState {
+  unsigned* sync = nullptr;  // SYNC_WORDS device words
+  void* area = nullptr;      // granules of eager calls
+  size_t area_bytes = 0;
 };
-std::mutex g_sync_mu;
-std::map<std::pair<int, hipStream_t>, SyncBlock> g_sync;
+std::mutex g_fu_mu;
+std::map<std::pair<int, hipStream_t>, StreamState> g_fu;
+unsigned g_epoch = 1;                 // last epoch handed out (guarded by g_fu_mu)
+unsigned* g_err_host = nullptr;       // host-mapped error word
+unsigned* g_err_host_dev = nullptr;   // its device address
+unsigned g_spin_max = SPIN_MAX;       // vrvq_rvq_debug (timeout test)
+unsigned g_stall = 0;
 constexpr unsigned EPOCH_RESET = 1u << 24;  // 64 epoch + stage stays below 2^32
 
-bool sync_for_launch(hipStream_t st, unsigned** dev, unsigned* epoch) {
+struct FusedLaunch {
+  unsigned* sync = nullptr;
+  unsigned epoch = 0;
+  char* area = nullptr;  // granule area of this launch (zeroed by memset nodes under capture)
+};
+
+// Sync block, epoch and granule area for one fused launch of `bytes` granules on st; false:
+// the fused launch cannot run now (the caller takes another path).
+bool fused_prepare(hipStream_t st, size_t bytes, void* caller_ws, size_t caller_bytes,
+                   FusedLaunch* L) {
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
   const bool capturing = cs != hipStreamCaptureStatusNone;
-  std::lock_guard<std::mutex> guard(g_sync_mu);
-  SyncBlock& sb = g_sync[{device, st}];
-  const size_t bytes = SYNC_WORDS * sizeof(unsigned);
-  if (!sb.dev) {
-    if (capturing) return false;  // no allocation inside a capture: three launches this time
-    if (hipMalloc(&sb.dev, bytes) != hipSuccess) {
-      sb.dev = nullptr;
+  std::lock_guard<std::mutex> guard(g_fu_mu);
+  if (!g_err_host && !capturing) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+      g_err_host = static_cast<unsigned*>(h);
+      __atomic_store_n(g_err_host, 0u, __ATOMIC_RELAXED);
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) g_err_host_dev = static_cast<unsigned*>(d);
+    }
+  }
+  StreamState& ss = g_fu[{device, st}];
+  const size_t sync_bytes = SYNC_WORDS * sizeof(unsigned);
+  if (!ss.sync) {
+    if (capturing) return false;  // no allocation inside a capture: another path this time
+    if (hipMalloc(&ss.sync, sync_bytes) != hipSuccess) {
+      ss.sync = nullptr;
       return false;
     }
-    if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
+    if (hipMemsetAsync(ss.sync, 0, sync_bytes, st) != hipSuccess) return false;
   }
   if (capturing) {
-    if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
-    *epoch = 1;
+    if (!caller_ws || caller_bytes < bytes) return false;
+    if (hipMemsetAsync(ss.sync, 0, sync_bytes, st) != hipSuccess ||
+        hipMemsetAsync(caller_ws, 0, bytes, st) != hipSuccess)
+      return false;
+    L->area = static_cast<char*>(caller_ws);
+    L->epoch = 1;
   } else {
-    if (++sb.epoch >= EPOCH_RESET) {
-      if (hipMemsetAsync(sb.dev, 0, bytes, st) != hipSuccess) return false;
-      sb.epoch = 2;
+    if (ss.area_bytes < bytes) {
+      if (ss.area) {
+        if (hipStreamSynchronize(st) != hipSuccess) return false;
+        (void)hipFree(ss.area);
+        ss.area = nullptr;
+        ss.area_bytes = 0;
+      }
+      const size_t want = bytes + bytes / 4;
+      if (hipMalloc(&ss.area, want) != hipSuccess) {
+        ss.area = nullptr;
+        return false;
+      }
+      if (hipMemsetAsync(ss.area, 0, want, st) != hipSuccess) return false;
+      ss.area_bytes = want;
     }
-    *epoch = sb.epoch;
+    if (++g_epoch >= EPOCH_RESET) {
+      g_epoch = 2;
+      for (auto& kv : g_fu)
+        if (kv.second.area) (void)hipMemsetAsync(kv.second.area, 0, kv.second.area_bytes, kv.first.second);
+    }
+    L->area = static_cast<char*>(ss.area);
+    L->epoch = g_epoch;
   }
-  *dev = sb.dev;
+  L->sync = ss.sync;
   return true;
 }
 
-// Clips per fused launch: every workgroup (2 per clip and part) resident at once, so that no
-// waiting workgroup can hold the slot of one it waits for (occupancy query, cached).
-template <int NM, bool PJ3>
-int fused_clip_capacity(size_t lds) {
+// Clips per fused launch: every workgroup resident at once, so that no waiting workgroup can
+// hold the slot of one it waits for (occupancy query with the launch's dynamic LDS, after the
+// attribute that allows it; cached per device, kernel and LDS size).
+int fused_clip_capacity(const void* kern, size_t lds, int wg_per_clip) {
   static std::mutex mu;
-  static std::map<std::pair<int, size_t>, int> cache;
+  static std::map<std::tuple<int, const void*, size_t>, int> cache;
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return 0;
   std::lock_guard<std::mutex> guard(mu);
-  auto it = cache.find({device, lds});
-  if (it != cache.end()) return it->second;
-  int cus = 0, per = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rvq_fused_kernel<NM, PJ3>, CH_NT, lds) !=
-          hipSuccess)
-    cus = per = 0;
-  const int clips = min(FU_CLIPS_MAX, cus * per / (2 * FU_NP));
-  cache[{device, lds}] = clips;
-  return clips;
+  const auto key = std::make_tuple(device, kern, lds);
+  auto it = cache.find(key);
+  int per_cu = 0;
+  if (it != cache.end()) {
+    per_cu = it->second;
+  } else {
+    int cus = 0, per = 0;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, CH_NT, lds) != hipSuccess)
+      cus = per = 0;
+    per_cu = cus * per;  // resident workgroups on the device
+    cache[key] = per_cu;
+  }
+  return per_cu / wg_per_clip;
 }
 
 constexpr int FUSED_NA = -1;  // the fused launch does not apply: take the three launches
@@ -1546,74 +1855,153 @@ struct LaunchTimer {
 };
 LaunchTimer g_timer;
 
+template <typename K>
+int launch_timed(K kern, unsigned grid, size_t lds, hipStream_t st, const FusedArgs& f) {
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (g_timer.next(&ev0, &ev1))
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(CH_NT), lds, st, ev0, ev1, 0, f);
+  else
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(CH_NT), lds, st, f);
+  return vrvq_launch_status();
+}
+
+// Chunk of clips [b0, b0 + bc) of a fused launch: the outputs and inputs offset to it.
+void fused_chunk_args(FusedArgs& f, int b0, int bc, int frames, int nq, int F, const float* z,
+                      const float* imp, int64_t* codes, float* latents, float* loss_pf,
+                      float* z_q_is, float* z_q, float* mask) {
+  const size_t DT = (size_t)RD * frames;
+  ChainArgs& c = f.c;
+  c.B = bc;
+  c.T = frames;
+  c.nq = nq;
+  c.F = F;
+  c.NF = bc * frames;
+  c.imp = imp ? imp + (size_t)b0 * frames : nullptr;
+  c.codes = codes + (size_t)b0 * nq * frames;
+  c.latents = latents + (size_t)b0 * nq * RCD * frames;
+  c.loss_pf = loss_pf + (size_t)b0 * nq * frames;
+  c.zst = nullptr;
+  c.mask = mask ? mask + (size_t)b0 * nq * frames : nullptr;
+  c.stamps = nullptr;
+  f.z = z + b0 * DT;
+  f.z_q_is = z_q_is ? z_q_is + (size_t)b0 * nq * DT : nullptr;
+  f.z_q = z_q + b0 * DT;
+  f.err_host = g_err_host_dev;
+  f.spin_max = g_spin_max;
+  f.stall = g_stall;
+  f.stamps = g_fstamps;
+  f.dbg = g_fdbg;
+}
+
+size_t zsh_bytes(int bc, int nq, int P) { return (size_t)bc * nq * P * FU_ROWS * RCD * 8; }
+
 template <int NM, bool PJ3>
 int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* z,
                     const float* imp, int64_t* codes, float* latents, float* loss_pf,
-                    float* z_q_is, float* z_q, float* mask, float* ws, hipStream_t st) {
+                    float* z_q_is, float* z_q, float* mask, float* ws, size_t ws_bytes,
+                    hipStream_t st) {
   const int F = (frames + FU_NP - 1) / FU_NP;
   size_t lds = (size_t)ChainLds(nq, F, 256 * NM).total * sizeof(float);
   const size_t lds_pj = PJ3 ? (size_t)PJ3_LDS : (size_t)PJ_CPS * PJ2_LD * sizeof(float);
   if (lds < lds_pj) lds = lds_pj;
   if (lds > 80 * 1024) return FUSED_NA;
-  const int cap = fused_clip_capacity<NM, PJ3>(lds);
+  const void* kern = (const void*)rvq_fused_kernel<NM, PJ3>;
+  const int cap = min(FU_CLIPS_MAX, fused_clip_capacity(kern, lds, 2 * FU_NP));
   if (cap < 1) return FUSED_NA;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)rvq_fused_kernel<NM, PJ3>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-  }
   const int bc_max = min(batch, cap);
-  float* part = ws;  // tagged granules: 2 floats per partial
-  unsigned long long* zsh =
-      reinterpret_cast<unsigned long long*>(ws + 2 * part_floats((long long)bc_max * frames, nq));
-  const size_t DT = (size_t)RD * frames;
+  const size_t part_b = 2 * part_floats((long long)bc_max * frames, nq) * sizeof(float);
+  const size_t need = part_b + zsh_bytes(bc_max, nq, FU_NP);
   for (int b0 = 0; b0 < batch; b0 += bc_max) {
     const int bc = min(bc_max, batch - b0);
     FusedArgs f = f0;
-    if (!sync_for_launch(st, &f.sync, &f.epoch)) {
+    FusedLaunch L;
+    if (!fused_prepare(st, need, ws, ws_bytes, &L)) {
       if (b0 == 0) return FUSED_NA;
       return VRVQ_ERR_UNSUPPORTED;  // cannot happen after a first successful chunk
     }
-    ChainArgs& c = f.c;
-    c.part = part;
-    c.B = bc;
-    c.T = frames;
-    c.nq = nq;
-    c.F = F;
-    c.NF = bc * frames;
-    c.imp = imp ? imp + (size_t)b0 * frames : nullptr;
-    c.codes = codes + (size_t)b0 * nq * frames;
-    c.latents = latents + (size_t)b0 * nq * RCD * frames;
-    c.loss_pf = loss_pf + (size_t)b0 * nq * frames;
-    c.zst = nullptr;
-    c.mask = mask ? mask + (size_t)b0 * nq * frames : nullptr;
-    c.stamps = nullptr;
-    f.z = z + b0 * DT;
-    f.z_q_is = z_q_is ? z_q_is + (size_t)b0 * nq * DT : nullptr;
-    f.z_q = z_q + b0 * DT;
-    f.zsh = zsh;
-    f.zsh_bytes = (int)((size_t)bc * nq * FU_NP * FU_ROWS * RCD * 8);
-    if (f.epoch == 1) {
-      // captured launch: every replay carries epoch 1, so the previous replay's granules would
-      // pass the tag checks -- zero them first (memset nodes of the graph)
-      if (hipMemsetAsync(zsh, 0, (size_t)f.zsh_bytes, st) != hipSuccess ||
-          hipMemsetAsync(part, 0, 2 * part_floats((long long)bc * frames, nq) * sizeof(float),
-                         st) != hipSuccess)
-        return VRVQ_ERR_ARG;
-    }
-    f.stamps = g_fstamps;
-    f.dbg = g_fdbg;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (g_timer.next(&ev0, &ev1))
-      hipExtLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
-                            dim3(CH_NT), lds, st, ev0, ev1, 0, f);
-    else
-      hipLaunchKernelGGL((rvq_fused_kernel<NM, PJ3>), dim3((unsigned)(2 * bc * FU_NP)),
-                         dim3(CH_NT), lds, st, f);
-    const int rc = vrvq_launch_status();
+    fused_chunk_args(f, b0, bc, frames, nq, F, z, imp, codes, latents, loss_pf, z_q_is, z_q, mask);
+    f.sync = L.sync;
+    f.epoch = L.epoch;
+    f.c.part = reinterpret_cast<float*>(L.area);  // tagged granules: 2 floats per partial
+    f.zsh = reinterpret_cast<unsigned long long*>(L.area + part_b);
+    f.zsh_bytes = (int)zsh_bytes(bc, nq, FU_NP);
+    f.P = FU_NP;
+    f.n_fb = 1;
+    const int rc = launch_timed(rvq_fused_kernel<NM, PJ3>, (unsigned)(2 * bc * FU_NP), lds, st, f);
     if (rc) return rc;
   }
   return 0;
+}
+
+// Frames per chain part of rvq_fm_kernel: T <= 128 (one expansion frame block per clip): 8
+// parts of ceil(T / 8); longer clips: 16 frames -- or fewer wherever the chain's LDS would not
+// fit twice per CU (beside an expansion workgroup): nq = 32 at T > 88.
+int fm_frames_per_part(int frames, int nq, int N) {
+  const int F0 = frames <= FU_FB ? (frames + 7) / 8 : FU_ROWS;
+  for (int F = F0; F >= 1; --F)
+    if (fm_lds_bytes(nq, F, N) <= 80 * 1024) return F;
+  return 0;
+}
+
+template <int NM>
+int launch_fm_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* zt,
+                 const float* imp, int64_t* codes, float* latents, float* loss_pf,
+                 float* z_q_is, float* z_q, float* mask, void* ws, size_t ws_bytes,
+                 hipStream_t st) {
+  const int F = fm_frames_per_part(frames, nq, 256 * NM);
+  if (F < 1) return VRVQ_ERR_UNSUPPORTED;
+  const int P = (frames + F - 1) / F;
+  const int n_fb = (frames + FU_FB - 1) / FU_FB;
+  const size_t lds = fm_lds_bytes(nq, F, 256 * NM);
+  if (lds > 80 * 1024) return VRVQ_ERR_UNSUPPORTED;
+  const void* kern = (const void*)rvq_fm_kernel<NM>;
+  const int wpc = P + (RD / FU_CB) * n_fb;  // workgroups per clip
+  const int cap = fused_clip_capacity(kern, lds, wpc);
+  if (cap < 1) return VRVQ_ERR_UNSUPPORTED;
+  int bc_max = min(batch, cap);
+  while (bc_max > 1 && zsh_bytes(bc_max, nq, P) > 0x7fffffffULL) --bc_max;
+  const size_t need = zsh_bytes(bc_max, nq, P);
+  for (int b0 = 0; b0 < batch; b0 += bc_max) {
+    const int bc = min(bc_max, batch - b0);
+    FusedArgs f = f0;
+    FusedLaunch L;
+    if (!fused_prepare(st, need, ws, ws_bytes, &L)) return VRVQ_ERR_UNSUPPORTED;
+    fused_chunk_args(f, b0, bc, frames, nq, F, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask);
+    f.sync = L.sync;
+    f.epoch = L.epoch;
+    f.c.part = nullptr;
+    f.zsh = reinterpret_cast<unsigned long long*>(L.area);
+    f.zsh_bytes = (int)zsh_bytes(bc, nq, P);
+    f.P = P;
+    f.n_fb = n_fb;
+    const int rc = launch_timed(rvq_fm_kernel<NM>, (unsigned)(bc * wpc), lds, st, f);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// W_in planes of rvq_fm_kernel in the 16x16x32 A-fragment order: w3in[ks][plane][rt][lane] =
+// 8 bf16 of row r = 16 rt + (lane & 15), channels 32 ks + 8 (lane >> 4) .. +7 (zero rows >= R).
+__global__ void rvq_pack_w_in_kernel(const float* __restrict__ w_in_t, int nq, u32x4* __restrict__ w3) {
+  const int n_rt = fm_nrt(nq), R = nq * RCD;
+  const int total = 32 * 3 * n_rt * 64;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int lane = o & 63;
+    int q = o >> 6;
+    const int rt = q % n_rt;
+    q /= n_rt;
+    const int plane = q % 3, ks = q / 3;
+    const int r = rt * 16 + (lane & 15), c0 = 32 * ks + 8 * (lane >> 4);
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = r < R ? w_in_t[((size_t)(r >> 3) * RD + c0 + u) * RCD + (r & 7)] : 0.0f;
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rvq_split3x2(v[2 * u], v[2 * u + 1], h[u], m[u], l[u]);
+    w3[o] = plane == 0 ? u32x4{h[0], h[1], h[2], h[3]}
+          : plane == 1 ? u32x4{m[0], m[1], m[2], m[3]} : u32x4{l[0], l[1], l[2], l[3]};
+  }
 }
 
 }  // namespace
@@ -1696,7 +2084,7 @@ extern "C" int vrvq_rvq_expand(const float* zst, int batch, int dim, int frames,
                                float level, float* z_q_is, float* z_q, float* mask,
                                vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(zst && w_out && b_out && z_q);
-  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim > 0);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim >= 4);
   if (cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
   return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q, mask,
                        as_stream(stream));
@@ -1707,7 +2095,7 @@ extern "C" int vrvq_rvq_expand_masked(const float* zst, int batch, int dim, int 
                                       const float* mask, float* z_q_is, float* z_q,
                                       vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(zst && w_out && b_out && mask && z_q);
-  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim > 0);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && dim >= 4);
   if (cdim != RCD) return VRVQ_ERR_UNSUPPORTED;
   return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, nullptr, 1.0f, z_q_is, z_q,
                        nullptr, as_stream(stream), mask);
@@ -1763,10 +2151,10 @@ extern "C" int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code) {
   if (hipGetDevice(&device) != hipSuccess) return VRVQ_ERR_ARG;
   unsigned* dev = nullptr;
   {
-    std::lock_guard<std::mutex> guard(g_sync_mu);
-    auto it = g_sync.find({device, st});
-    if (it == g_sync.end() || !it->second.dev) return 0;
-    dev = it->second.dev;
+    std::lock_guard<std::mutex> guard(g_fu_mu);
+    auto it = g_fu.find({device, st});
+    if (it == g_fu.end() || !it->second.sync) return 0;
+    dev = it->second.sync;
   }
   unsigned v = 0;
   hipError_t e = hipMemcpyAsync(&v, dev + SYNC_ERR, sizeof(v), hipMemcpyDeviceToHost, st);
@@ -1774,6 +2162,22 @@ extern "C" int vrvq_rvq_sync_error(vrvq_stream_t stream, int* code) {
   if (e == hipSuccess && v) e = hipMemsetAsync(dev + SYNC_ERR, 0, sizeof(unsigned), st);
   if (e != hipSuccess) return (int)e;
   *code = (int)v;
+  if (v && g_err_host) __atomic_store_n(g_err_host, 0u, __ATOMIC_RELAXED);  // reported here
+  return 0;
+}
+
+extern "C" int vrvq_rvq_pending_error(int* code) {
+  VRVQ_CHECK_ARG(code);
+  *code = 0;
+  std::lock_guard<std::mutex> guard(g_fu_mu);
+  if (g_err_host) *code = (int)__atomic_exchange_n(g_err_host, 0u, __ATOMIC_RELAXED);
+  return 0;
+}
+
+extern "C" int vrvq_rvq_debug(unsigned spin_max, unsigned stall) {
+  std::lock_guard<std::mutex> guard(g_fu_mu);
+  g_spin_max = spin_max ? spin_max : SPIN_MAX;
+  g_stall = stall;
   return 0;
 }
 
@@ -1807,11 +2211,12 @@ extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, i
     f.b_out = b_out;
     int rc = FUSED_NA;
     const bool pj3 = project_variant() == 3;
+    const size_t wsb = (size_t)workspace_bytes;
 #define VRVQ_FUSED_CASE(NMV)                                                                    \
   rc = pj3 ? launch_fused_nm<NMV, true>(f, batch, frames, nq, z, imp, codes, latents, loss_pf,  \
-                                        z_q_is, z_q, mask, part, st)                          \
+                                        z_q_is, z_q, mask, part, wsb, st)                     \
            : launch_fused_nm<NMV, false>(f, batch, frames, nq, z, imp, codes, latents, loss_pf, \
-                                         z_q_is, z_q, mask, part, st)
+                                         z_q_is, z_q, mask, part, wsb, st)
     switch (ncode / 256) {
       case 1: VRVQ_FUSED_CASE(1); break;
       case 2: VRVQ_FUSED_CASE(2); break;
@@ -1828,4 +2233,60 @@ extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, i
   if (rc) return rc;
   return launch_expand(zst, batch, dim, frames, nq, w_out, b_out, imp, level, z_q_is, z_q,
                        nullptr, st);
+}
+
+extern "C" int vrvq_rvq_w_in_planes_size(int nq, int dim, int cdim, long long* n_u16) {
+  VRVQ_CHECK_ARG(n_u16 && nq > 0);
+  if (dim != RD || cdim != RCD || nq > CH_NQMAX) return VRVQ_ERR_UNSUPPORTED;
+  *n_u16 = 32LL * 3 * fm_nrt(nq) * 64 * 8;
+  return 0;
+}
+
+extern "C" int vrvq_rvq_pack_w_in(const float* w_in_t, int nq, int dim, int cdim, uint16_t* w3in,
+                                  vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(w_in_t && w3in && nq > 0);
+  if (dim != RD || cdim != RCD || nq > CH_NQMAX) return VRVQ_ERR_UNSUPPORTED;
+  const int total = 32 * 3 * fm_nrt(nq) * 64;
+  hipLaunchKernelGGL(rvq_pack_w_in_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     as_stream(stream), w_in_t, nq, reinterpret_cast<u32x4*>(w3in));
+  return vrvq_launch_status();
+}
+
+extern "C" int vrvq_rvq_workspace_fm(int batch, int frames, int nq, int ncode, long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0 && ncode > 0);
+  const int F = fm_frames_per_part(frames, nq, ncode);
+  if (F < 1) return VRVQ_ERR_UNSUPPORTED;
+  const int P = (frames + F - 1) / F;
+  *bytes = (long long)zsh_bytes(batch, nq, P);
+  return 0;
+}
+
+extern "C" int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frames, int nq,
+                                  int ncode, int cdim, const uint16_t* w3in, const float* b_in,
+                                  const float* cb, const float* cbf, const float* c2,
+                                  const float* w_out, const float* b_out, const float* mcol,
+                                  const float* qb, const float* imp, float level, int64_t* codes,
+                                  float* latents, float* loss_pf, float* z_q_is, float* z_q,
+                                  float* mask, void* workspace, long long workspace_bytes,
+                                  vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(zt && w3in && b_in && cb && cbf && c2 && w_out && b_out && mcol && qb &&
+                 codes && latents && loss_pf && z_q);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && workspace_bytes >= 0);
+  VRVQ_CHECK_ARG(((uintptr_t)workspace & 15) == 0);
+  if (!rvq_shape_ok(dim, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  FusedArgs f{};
+  ChainArgs& c = f.c;
+  c.b_in = b_in; c.qb = qb; c.mcol = mcol; c.cb = cb; c.cbf = cbf; c.c2 = c2;
+  c.level = level;
+  f.w3in = reinterpret_cast<const u32x4*>(w3in);
+  f.w_out = w_out;
+  f.b_out = b_out;
+  hipStream_t st = as_stream(stream);
+  const size_t wsb = (size_t)workspace_bytes;
+  switch (ncode / 256) {
+    case 1: return launch_fm_nm<1>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    case 2: return launch_fm_nm<2>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    case 3: return launch_fm_nm<3>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    default: return launch_fm_nm<4>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+  }
 }

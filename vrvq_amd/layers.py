@@ -125,6 +125,20 @@ class WNConv1d(nn.Module):
                           want_raw=want_raw, w_x3=self.prepared_x3())
 
 
+    def forward_fm(self, x: torch.Tensor, snake: Optional[Snake1d] = None) -> torch.Tensor:
+        """conv(snake(x)) + bias (stride 1) as a FRAME-MAJOR (B, T, Cout) tensor (the RVQ's
+        zt layout, include/vrvq.h vrvq_conv1d_fm); same values as forward."""
+        if self.stride[0] != 1:
+            raise RuntimeError("forward_fm: stride-1 convs only")
+        wp, _ = self.prepared()
+        alpha = inv = None
+        if snake is not None:
+            alpha, inv = snake.prepared()
+        return ops.conv1d_fm(x, wp, self.out_channels, self.kernel_size[0], self.padding[0],
+                             self.dilation[0], bias=self.bias.detach(), alpha=alpha,
+                             inv_alpha=inv, w_x3=self.prepared_x3())
+
+
 class WNConvTranspose1d(nn.Module):
     """Weight-normalised ConvTranspose1d (models/layers.py:21-22); norm over dim 0 = Cin."""
 

@@ -8,6 +8,7 @@ libvrvq_hip.so (see ops.py); the modules here hold parameters and orchestrate la
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Union
 
 import numpy as np
@@ -33,7 +34,10 @@ class Encoder(nn.Module):
         self.block = nn.Sequential(*blocks)
         self.valid = False  # padding=False (CodecMixin.padding): unpadded convs
 
-    def forward(self, x, return_feat: bool = False):
+    def forward(self, x, return_feat: bool = False, frame_major: bool = False):
+        """frame_major: z comes back as the (B, D, T) view of a frame-major (B, T, D) tensor,
+        written that way by the last conv's epilogue (the layout the fused RVQ reads, see
+        _is_frame_major); the values are the same."""
         if self.training:  # autograd path (vrvq_amd/train.py)
             if self.valid:
                 raise NotImplementedError("padding=False is an inference (compress) mode")
@@ -61,7 +65,10 @@ class Encoder(nn.Module):
             r = self.block[i].run(x, x_snk, nxt, want_raw=True)
             x, x_snk = (r, None) if last else r
         feat = x  # output of block index n-3 (the last EncoderBlock), models/dac_vrvq.py:43-44
-        out = self.block[n - 1](x, snake=self.block[n - 2])
+        if frame_major:
+            out = self.block[n - 1].forward_fm(x, snake=self.block[n - 2]).transpose(1, 2)
+        else:
+            out = self.block[n - 1](x, snake=self.block[n - 2])
         return (out, feat) if return_feat else out
 
 
@@ -145,12 +152,31 @@ class VectorQuantize(nn.Module):
         Returns z_q, commitment_loss, codebook_loss, indices, z_e as the reference does
         (losses per frame (B, T) if loss_per_frame else per item (B,))."""
         st = _stack_stages([self], z.device)
-        codes, latents, loss_pf, _, z_q, _ = ops.rvq_encode(
-            z.contiguous(), *st.codes_args(), want_z_q_is=False, want_mask=False)
+        codes, latents, loss_pf, _, z_q, _ = _rvq_encode(z, st, want_z_q_is=False,
+                                                          want_mask=False)
         loss = loss_pf[:, 0, :]
         if not loss_per_frame:
             loss = loss.mean(1)
         return z_q, loss, loss.clone(), codes[:, 0, :], latents
+
+
+# The encoder hands z to the quantizer frame-major (vrvq_rvq_encode_fm: each chain part reads
+# its frames' contiguous rows and projects them itself) unless VRVQ_RVQ_FM=0 (A/B: z (B, D, T)
+# and vrvq_rvq_encode).
+RVQ_FM = os.environ.get("VRVQ_RVQ_FM", "1") != "0"
+
+
+def _is_frame_major(z: torch.Tensor) -> bool:
+    """z (B, D, T) is the transposed view of a contiguous (B, T, D) tensor."""
+    return z.dim() == 3 and not z.is_contiguous() and z.transpose(1, 2).is_contiguous()
+
+
+def _rvq_encode(z, st, **kw):
+    """ops.rvq_encode, or ops.rvq_encode_fm when z is a frame-major view."""
+    if _is_frame_major(z):
+        return ops.rvq_encode_fm(z.transpose(1, 2), st.w3in(), st.b_in, st.cb, st.cbf, st.c2,
+                                 st.w_out, st.b_out, st.mcol, st.qb, **kw)
+    return ops.rvq_encode(z.contiguous(), *st.codes_args(), **kw)
 
 
 class _Stacked:
@@ -180,8 +206,15 @@ class _Stacked:
         return (self.w_in_t, self.b_in, self.cb, self.cbf, self.c2, self.w_out, self.b_out,
                 self.mcol, self.qb)
 
+    def w3in(self):
+        """W_in planes of rvq_encode_fm (packed on first use)."""
+        if getattr(self, "_w3in", None) is None:
+            self._w3in = ops.rvq_pack_w_in(self.w_in_t)
+        return self._w3in
+
     def prefix(self, n):
         s = _Stacked.__new__(_Stacked)
+        s._w3in = None
         for k in ("w_in_t", "b_in", "cb", "cbn", "cbf", "c2", "w_out", "b_out", "qb"):
             setattr(s, k, getattr(self, k)[:n].contiguous())
         s.mcol = self.mcol[:n, :n].contiguous()
@@ -226,8 +259,8 @@ class ResidualVectorQuantize(nn.Module):
         st = self.stacked()
         if n < self.n_codebooks:
             st = st.prefix(n)
-        codes, latents, loss_pf, _, z_q, _ = ops.rvq_encode(
-            z.contiguous(), *st.codes_args(), want_z_q_is=False, want_mask=False)
+        codes, latents, loss_pf, _, z_q, _ = _rvq_encode(z, st, want_z_q_is=False,
+                                                          want_mask=False)
         loss = ops.masked_loss(loss_pf, None)  # sum_i mean_{b,t} loss_i (mask all-true in eval)
         return {"z_q": z_q, "codes": codes, "latents": latents,
                 "commitment_loss": loss, "codebook_loss": loss.clone()}
@@ -329,8 +362,8 @@ class VBRResidualVectorQuantize(ResidualVectorQuantize):
         else:
             imp_map, imp, lvl = None, None, 1.0
         # residual chain, z_q_is stream, importance mask, masked z_q
-        codes, latents, loss_pf, z_q_is, z_q, mask = ops.rvq_encode(
-            z.contiguous(), *st.codes_args(), imp=imp, level=lvl, want_z_q_is=want_z_q_is)
+        codes, latents, loss_pf, z_q_is, z_q, mask = _rvq_encode(
+            z, st, imp=imp, level=lvl, want_z_q_is=want_z_q_is)
         loss = ops.masked_loss(loss_pf, mask)
         return {
             "z_q": z_q,
@@ -502,7 +535,8 @@ class DAC_VRVQ(nn.Module, CodecMixin):
         `want_z_q_is=False` skips materialising the (B, Nq, D, T) per-codebook tensor when the
         caller does not need it (it is ~90 % of the quantizer's HBM traffic); the default keeps
         the reference's dict."""
-        z, feat = self.encoder(audio_data.contiguous(), return_feat=True)
+        fm = RVQ_FM and not self.training and not self.encoder.valid
+        z, feat = self.encoder(audio_data.contiguous(), return_feat=True, frame_major=fm)
         if self.model_type == "CBR":
             return self.quantizer(z, n_quantizers)
         return self.quantizer(z, n_quantizers, feat, level, want_z_q_is=want_z_q_is)
