@@ -107,6 +107,30 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
+/* vrvq_conv1d with the bf16 "planes" layouts of a Snake-activated operand (csrc/conv_pl.h):
+ *   y_snake_planes  (instead of y_snake) snake_out(y) as three bf16 planes [B][3][cout/8][tout][8]
+ *                   (v = h + m + l exactly: the split the x3 staging would make; cout % 8 == 0,
+ *                   16-byte aligned);
+ *   x_planes != 0   x is such a planes tensor [B][3][cin/8][tin][8] holding snake(x) (alpha must
+ *                   be NULL): the k7 "planes" tile (stride 1, pad 3 dil, w_x3 required,
+ *                   cin % 16 == 0, cout % 64 == 0 and >= 128), whose K-chunk stages are filled by
+ *                   LDS-DMA with no register staging; outputs bit-identical to the fp32-input
+ *                   x3 k7 pair tile on the same values.
+ * Used by the residual units' k7 -> k1 chain (models/layers.py:52-68). VRVQ_ERR_UNSUPPORTED
+ * for shapes outside those. */
+int vrvq_conv1d_ex(const void* x, int x_planes, int batch, int cin, int tin, const float* alpha,
+                   const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
+                   int cout_pad, int k, int stride, int pad, int dil, const float* bias,
+                   const float* residual, int epilogue, float* y, int tout,
+                   const float* alpha_out, const float* inv_alpha_out, float* y_snake,
+                   uint16_t* y_snake_planes, vrvq_stream_t stream);
+/* vrvq_conv_transpose1d_pad with snake_out(y) as planes (strides 2 / 4 / 8, cout % 8 == 0). */
+int vrvq_conv_transpose1d_ex(const float* x, int batch, int cin, int tin, const float* alpha,
+                             const float* inv_alpha, const float* w_packed, const uint16_t* w_x3,
+                             int cout, int cout_pad, int stride, int pad, const float* bias,
+                             float* y, const float* alpha_out, const float* inv_alpha_out,
+                             float* y_snake, uint16_t* y_snake_planes, vrvq_stream_t stream);
+
 /* vrvq_conv1d (stride 1, no residual / epilogue / output Snake) writing y FRAME-MAJOR:
  * y_fm[b][t][co] (tout x cout per clip, cout % 4 == 0, 16-byte aligned) -- the encoder's last
  * conv (models/dac_vrvq.py:34) producing z in the layout of vrvq_rvq_encode_fm's zt, straight

@@ -26,6 +26,10 @@ SIGNATURES = {
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
+    "vrvq_conv1d_ex": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I,
+                       _P, _I, _P, _P, _P, _P, _P],
+    "vrvq_conv_transpose1d_ex": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
+                                 _P, _P, _P],
     "vrvq_conv1d_fm": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
     "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],

@@ -40,7 +40,40 @@ struct ConvArgs {
   // Frame-major output yfm[B][ng][M] (y of the encoder's last conv as the RVQ's zt,
   // vrvq_conv1d_fm): written straight from the accumulators with the bias, instead of y.
   float* yfm;
+  // snake_o(y) as three bf16 planes ysp[B][3][cout / 8][ylen][8] (v = h + m + l exactly, the
+  // split the x3 staging would make of the same fp32 value) instead of fp32 ys: the operand of
+  // the planes k7 tile (conv_pl.h), which fills its LDS stages with LDS-DMA, no VALU.
+  unsigned short* ysp;
 };
+
+// v = h + m + l exactly (RNE at each step; conv_x3.h split3x2), two values per call
+__device__ __forceinline__ void split3x2_core(float v0, float v1, unsigned& h, unsigned& m,
+                                              unsigned& l) {
+  typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  const f32x2_ v = {v0, v1};
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_));
+  const f32x2_ hf = {__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+  const f32x2_ r = v - hf;
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2_));
+  const f32x2_ mf = {__uint_as_float(mu << 16), __uint_as_float(mu & 0xffff0000u)};
+  const f32x2_ s = r - mf;
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2_));
+}
+
+// Eight channels' snake values at one position -> their 16-B groups of the three planes.
+__device__ __forceinline__ void store_planes8(unsigned short* ysp, size_t plane_stride,
+                                              size_t off, const float (&v)[8]) {
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) split3x2_core(v[2 * u], v[2 * u + 1], h[u], m[u], l[u]);
+  *reinterpret_cast<u32x4_*>(ysp + off) = u32x4_{h[0], h[1], h[2], h[3]};
+  *reinterpret_cast<u32x4_*>(ysp + plane_stride + off) = u32x4_{m[0], m[1], m[2], m[3]};
+  *reinterpret_cast<u32x4_*>(ysp + 2 * plane_stride + off) = u32x4_{l[0], l[1], l[2], l[3]};
+}
 
 template <int KS, int BM, int BN>
 struct ChunkCfg {
@@ -341,7 +374,34 @@ __device__ __forceinline__ void conv_epilogue(
     }
     __syncthreads();
     const int p0 = n0 + pass * BNP;  // first GEMM column of this pass
-    if (a.up == 0) {
+    if (a.up == 0 && a.ysp) {
+      // planes output: item = (channel octet, column); per item the eight rows' conv_epilogue
+      // expressions (bias, residual, act, y) and snake_o, then the 16-B groups of the planes.
+      // Consecutive lanes take consecutive columns: every plane store is 1 KB per wave.
+      const int ncols = min(BNP, a.ng - p0);
+      const int nocts = mrows >> 3;  // M % 8 == 0 (the launcher checks)
+      const size_t pstride = (size_t)(a.cout >> 3) * a.ylen * 8;  // bf16 per plane
+      for (int e = tid; e < nocts * BNP; e += NT) {
+        const int o = e / BNP, nl = e - o * BNP;
+        if (nl >= ncols) continue;
+        const int n = p0 + nl;
+        float v[8], al[8], ia[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int m = m0 + 8 * o + u;
+          v[u] = ct[(8 * o + u) * BNP + nl] + (a.bias ? a.bias[m] : 0.0f);
+          const size_t ob = ((size_t)b * a.cout + m) * a.ylen + n;
+          if (a.res) v[u] = a.res[ob] + v[u];
+          v[u] = apply_epi(v[u], a.epi);
+          if (a.y) a.y[ob] = v[u];
+          al[u] = a.alpha_o[m];
+          ia[u] = a.inv_alpha_o[m];
+        }
+        snake_n<8>(v, al, ia);
+        const size_t off = ((((size_t)b * 3) * (a.cout >> 3) + ((m0 >> 3) + o)) * a.ylen + n) * 8;
+        store_planes8(a.ysp, pstride, off, v);
+      }
+    } else if (a.up == 0) {
       // Each thread owns 4 consecutive columns per step; U steps are loaded (accumulator
       // tile, bias, residual, next-layer alpha) before anything is stored, so the global
       // loads of a step group are in flight together.
@@ -471,7 +531,39 @@ __device__ __forceinline__ void conv_epilogue(
           }
         }
       };
-      if (a.up == 8 && BM % 8 == 0) walk4(std::integral_constant<int, 8>{});
+      // planes output (snake_o(y) for a planes k7 consumer): item = (channel octet, output
+      // sample), the walk4 expressions per channel, consecutive lanes on consecutive samples
+      auto walk_planes = [&](auto up_c) {
+        constexpr int UP = decltype(up_c)::value;
+        const int co0 = m0 / UP, nco = min(BM / UP, a.cout - co0);  // nco % 8 == 0 (launcher)
+        const int tl_n = BNP * UP;
+        const size_t pstride = (size_t)(a.cout >> 3) * a.ylen * 8;
+        for (int e = tid; e < (nco >> 3) * tl_n; e += NT) {
+          const int o = e / tl_n, tl = e - o * tl_n;
+          const int nl = tl / UP, ph = tl - nl * UP;
+          const int t = (p0 + nl) * UP + ph - a.up_pad;
+          if (p0 + nl >= a.ng || t < 0 || t >= a.ylen) continue;
+          float v[8], al[8], ia[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int co = co0 + 8 * o + u;
+            v[u] = ct[((8 * o + u) * UP + ph) * BNP + nl];
+            if (a.bias) v[u] = v[u] + a.bias[co];
+            if (a.y) a.y[((size_t)b * a.cout + co) * a.ylen + t] = v[u];
+            al[u] = a.alpha_o[co];
+            ia[u] = a.inv_alpha_o[co];
+          }
+          snake_n<8>(v, al, ia);
+          const size_t off =
+              ((((size_t)b * 3) * (a.cout >> 3) + ((co0 >> 3) + o)) * a.ylen + t) * 8;
+          store_planes8(a.ysp, pstride, off, v);
+        }
+      };
+      if (a.ysp) {
+        if (a.up == 8 && BM % 8 == 0) walk_planes(std::integral_constant<int, 8>{});
+        else if (a.up == 4 && BM % 4 == 0) walk_planes(std::integral_constant<int, 4>{});
+        else if (a.up == 2) walk_planes(std::integral_constant<int, 2>{});
+      } else if (a.up == 8 && BM % 8 == 0) walk4(std::integral_constant<int, 8>{});
       else if (a.up == 4 && BM % 4 == 0) walk4(std::integral_constant<int, 4>{});
       else if (a.up == 2) walk4(std::integral_constant<int, 2>{});
       else walk(std::integral_constant<int, 0>{});

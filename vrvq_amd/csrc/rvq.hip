@@ -1173,25 +1173,56 @@ struct FusedArgs {
 
 // Expansion workgroup (clip b, frames [128 fb, +128), channels [128 cb, +128)): wave w =
 // 32-channel tile (w & 3) x 32-frame tiles {w >> 2, (w >> 2) + 2} of the block; per stage four
-// v_mfma_f32_32x32x2_f32 per tile (K = 8: W_out x zst, the k-ordered fma chain) and the bias as
-// one VALU add -- rvq_expand_kernel's expression (dot8(W, zst) + bias) with one matrix-core op
-// fewer per tile and stage than the bias-as-9th-k form. Every wave runs on its own (no barrier).
-// The stage's zst rows are tagged granules (the chain's S2 stores): a wave loads stage i + 1's
-// granules (and W_out / b_out rows) speculatively BEFORE stage i's z_q_is stores and checks
-// their tags when it gets there -- vmcnt retires in order, so a load issued after the stores
-// would wait for them to drain (with flag words trailing the data the workgroup ran ~4 us per
-// stage, bound by its own store queue: profiles/r04d_fused_timeline.txt). Rows whose tags are
-// not this call's stage yet are re-read until they are (bounded; on the bound the tile's
-// outputs are NaN).
+// v_mfma_f32_32x32x2_f32 per tile, D[channel][frame] = sum_k W_out[channel][k] zst[frame][k]
+// (rvq_expand_kernel's k-ordered products). D leaves the MFMA with one frame per lane and four
+// consecutive channels per register quad; a 4 x 4 transpose inside each lane quad (two DPP
+// quad_perm exchanges) turns that into four consecutive FRAMES of one channel per register
+// quad, so z_q_is / z_q leave as 16-B stores that cover 8 whole 128-B row segments per wave
+// instruction (r04's 4-B stores needed 4x the instructions; 16-B stores straight from the
+// frame-major D orientation touched 32 rows per instruction and ran slower still:
+// profiles/r05i_stamps.log). Bias and mask are then per register (the three-launch kernel's
+// expressions, per element). Every wave runs on its own (no barrier). The stage's zst rows are
+// tagged granules (the chain's S2 stores): a wave loads stage i + 1's granules (and its
+// W_out row / biases) speculatively BEFORE stage i's stores and checks their tags when it gets
+// there -- vmcnt retires in order, so a load issued after the stores would wait for them to
+// drain (profiles/r04d_fused_timeline.txt). Rows whose tags are not this call's stage yet are
+// re-read until they are (bounded; on the bound the tile's outputs are NaN).
+// What bounds a stage is the z_q_is write stream (11.4 MB per stage at B = 32, ~4 us: ~2.9 TB/s
+// next to the chain's traffic); without z_q_is the expansion keeps pace with the chain
+// (profiles/r05j_stamps_nozqis.log), and unconditional buffer stores -- so that no load ever
+// waits for the stores to drain -- changed nothing (profiles/r05l_stamps_unconditional_stores.log).
 struct ExOps {
   float4 w0, w1;
+  float bb[4];    // b_out of the lane's four output channels (one per register quad)
   u32x4 z[2][2];  // per frame tile: 4 granules {zst k = 2 s + h, tag}, s = 0..3
 };
 
-// sm: the launch's LDS (unused by the expansion role otherwise): b_out of the workgroup's 128
-// channels for every stage, so a lane reads the bias of its 16 accumulator rows as four
-// broadcast ds_read_b128 per stage instead of keeping them in registers a stage ahead.
+// 4 x 4 transpose inside each lane quad: lane 4 g + k, register 4 qd + u holds E(u, k) on
+// entry and E(k, u) on exit (E(row, column) of the quad's 4 x 4 block). Two butterfly steps,
+// each swapping one index bit of the register with the same bit of the lane.
+__device__ __forceinline__ void quad_transpose(f32x16& q, int lane) {
+  const bool o1 = lane & 1, o2 = lane & 2;
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // register pairs (0, 1), (2, 3): lanes k ^ 1
+      const int r0 = 4 * qd + 2 * p, r1 = r0 + 1;
+      const float snd = o1 ? q[r0] : q[r1];
+      const float got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), 0xB1, 0xF, 0xF, false));
+      if (o1) q[r0] = got; else q[r1] = got;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // register pairs (0, 2), (1, 3): lanes k ^ 2
+      const int r0 = 4 * qd + p, r1 = r0 + 2;
+      const float snd = o2 ? q[r0] : q[r1];
+      const float got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), 0x4E, 0xF, 0xF, false));
+      if (o2) q[r0] = got; else q[r1] = got;
+    }
+  }
+}
+
 __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, float* sm) {
+  (void)sm;
   const int nq = f.c.nq, T = f.c.T, F = f.c.F;
   constexpr int NCB = RD / FU_CB;
   const int cb = e % NCB;
@@ -1207,23 +1238,38 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   const bool two = ft0 + 2 < n_ft;   // ... and a second
   const __amdgpu_buffer_rsrc_t zr =
       __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
-  int zoff[2];  // byte offset of this lane's 4 granules of stage 0
-  int tt[2];
-  bool tv[2];
-  float sc[2];
+  // after the transpose: lane (g = col >> 2, k = lane & 3, h), register 4 qd + u holds channel
+  // c0 + 8 qd + 4 h + k, frame tile_base + 4 g + u
+  const int chk = c0 + 4 * h + (lane & 3);  // + 8 qd
+  int zoff[2];    // byte offset of this lane's 4 granules of stage 0 (its B-operand frame col)
+  int tq[2];      // first of the lane's four output frames
+  unsigned nact[2];  // per output frame u: the number of active stages (mask = i < n), bytes
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int t = fb * FU_FB + (ft0 + 2 * j) * 32 + col;
-    tt[j] = t;
-    tv[j] = t < T && (j == 0 ? one : two);
-    const int tc = min(t, T - 1);
+    const int tb = fb * FU_FB + (ft0 + 2 * j) * 32;  // the tile's first frame
+    const int tc = min(tb + col, T - 1);
     const int p = tc / F, fr = tc - p * F;
     zoff[j] = ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
-    sc[j] = (f.c.imp && tv[j]) ? (f.c.imp[(size_t)b * T + tc] * f.c.level) * (float)nq : INFINITY;
+    tq[j] = tb + 4 * (col >> 2);
+    float sv[4];  // the loads first: one memory latency
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = min(tq[j] + u, T - 1);
+      sv[u] = f.c.imp ? (f.c.imp[(size_t)b * T + t] * f.c.level) * (float)nq : INFINITY;
+    }
+    unsigned w = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // mask[b,i,t] = (s - i >= 0) with s = (imp * level) * nq (models/utils.py:45-61). The
+      // fp32 difference rounds monotonically and 0 is exact, so that is s >= i: the first
+      // floor(s) + 1 stages (none for NaN or s < 0, all nq for s >= nq - 1 or CBR's inf)
+      const int n = sv[u] >= 0.0f ? (int)floorf(fminf(sv[u], (float)(nq - 1))) + 1 : 0;
+      w |= (unsigned)n << (8 * u);
+    }
+    nact[j] = w;
   }
   const int zstage = f.P * FU_ROWS * RCD * 8;  // bytes per stage
-  const int cr = c0 + col;  // A-operand row of this lane
-  const float* wp = f.w_out + (size_t)cr * RCD;
+  const float* wp = f.w_out + (size_t)(c0 + col) * RCD;  // A operand: channel row c0 + col
   const size_t wstride = (size_t)RD * RCD;
   const unsigned base = f.epoch * 64u;
   auto load_z = [&](int i, u32x4 (&z)[2][2]) {
@@ -1237,6 +1283,8 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   auto load = [&](int i, ExOps& o) {
     o.w0 = ld4(wp + i * wstride);
     o.w1 = ld4(wp + i * wstride + 4);
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) o.bb[qd] = f.b_out[(size_t)i * RD + chk + 8 * qd];
     load_z(i, o.z);
   };
   auto tagged = [&](const u32x4 (&z)[2][2], int i) -> bool {  // wave-uniform
@@ -1249,15 +1297,24 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
                z[j][1][3] == tag;
     return __builtin_amdgcn_ballot_w64(!good) == 0;
   };
+  // four consecutive frames of one channel: one 16-B store (rows of T floats are dword-
+  // aligned), elementwise at the clip's last, partial quad
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  auto store_quad = [&](float* row, int t, float v0, float v1, float v2, float v3) {
+    if (t + 4 <= T) {
+      *reinterpret_cast<f4u*>(row + t) = f4u{v0, v1, v2, v3};
+    } else {
+      if (t < T) row[t] = v0;
+      if (t + 1 < T) row[t + 1] = v1;
+      if (t + 2 < T) row[t + 2] = v2;
+    }
+  };
   f32x16 zq[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) zq[j][r] = 0.0f;
   ExOps cur;
-  float* bias_s = sm;  // [nq][FU_CB]
-  for (int k = threadIdx.x; k < nq * FU_CB; k += CH_NT)
-    bias_s[k] = f.b_out[(size_t)(k / FU_CB) * RD + cb * FU_CB + (k % FU_CB)];
   __shared__ int xdead_s;  // wave 0's stage-0 wait ran out (then no wave waits any more)
   bool dead = false;       // a wait ran out: no more waits (err recorded), outputs NaN
   // stage 0 lands after the chain's first stage: wave 0 alone watches its rows with a long
@@ -1295,8 +1352,6 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
     load(min(i + 1, nq - 1), nxt);
     const float wa[4] = {h ? cur.w0.y : cur.w0.x, h ? cur.w0.w : cur.w0.z,
                          h ? cur.w1.y : cur.w1.x, h ? cur.w1.w : cur.w1.z};
-    // bias of the accumulator rows (c0 + 4 h + (r & 3) + 8 (r >> 2)) of this lane
-    const float* brow = bias_s + i * FU_CB + (wave & 3) * 32 + 4 * h;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (!(j == 0 ? one : two)) break;
@@ -1314,36 +1369,35 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
 #ifdef VRVQ_STAMPS
       }
 #endif
+      quad_transpose(q, lane);
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float4 v = *reinterpret_cast<const float4*>(brow + 8 * qq);
-        q[4 * qq] = q[4 * qq] + v.x;
-        q[4 * qq + 1] = q[4 * qq + 1] + v.y;
-        q[4 * qq + 2] = q[4 * qq + 2] + v.z;
-        q[4 * qq + 3] = q[4 * qq + 3] + v.w;
-      }
-      if (dead)
+      for (int r = 0; r < 16; ++r) q[r] = dead ? __builtin_nanf("") : q[r] + cur.bb[r >> 2];
+      if (f.z_q_is) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) q[r] = __builtin_nanf("");
-      const float m = (sc[j] - (float)i >= 0.0f) ? 1.0f : 0.0f;  // models/utils.py:45-61
-      if (f.z_q_is && tv[j]) {
-        float* dst = f.z_q_is + (((size_t)b * nq + i) * RD + c0 + 4 * h) * T + tt[j];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = q[r];
+        for (int qd = 0; qd < 4; ++qd) {
+          float* row = f.z_q_is + (((size_t)b * nq + i) * RD + chk + 8 * qd) * T;
+          store_quad(row, tq[j], q[4 * qd], q[4 * qd + 1], q[4 * qd + 2], q[4 * qd + 3]);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) zq[j][r] = zq[j][r] + q[r] * m;
+      for (int r = 0; r < 16; ++r) {
+        const unsigned n = (nact[j] >> (8 * (r & 3))) & 0xffu;
+        const float m = (unsigned)i < n ? 1.0f : 0.0f;  // models/utils.py:45-61
+        zq[j][r] = zq[j][r] + q[r] * m;
+      }
     }
     cur = nxt;
   }
   FSTAMP(f.stamps, 40);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    if (tv[j]) {
-      float* dst = f.z_q + ((size_t)b * RD + c0 + 4 * h) * T + tt[j];
+    if (!(j == 0 ? one : two)) break;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        dst[(size_t)((r & 3) + 8 * (r >> 2)) * T] = dead ? __builtin_nanf("") : zq[j][r];
+    for (int qd = 0; qd < 4; ++qd) {
+      float* row = f.z_q + ((size_t)b * RD + chk + 8 * qd) * T;
+      const float d = dead ? __builtin_nanf("") : 0.0f;
+      store_quad(row, tq[j], zq[j][4 * qd] + d, zq[j][4 * qd + 1] + d, zq[j][4 * qd + 2] + d,
+                 zq[j][4 * qd + 3] + d);
     }
   }
 }

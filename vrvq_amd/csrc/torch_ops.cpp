@@ -164,7 +164,7 @@ const uint16_t* x3_ptr(const optional<Tensor>& w3, const Tensor& ref, int64_t ci
 std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef shape,
                                             const optional<Tensor>& alpha_out,
                                             const optional<Tensor>& inv_alpha_out,
-                                            bool want_raw) {
+                                            bool want_raw, bool no_ys = false) {
   TORCH_CHECK(alpha_out.has_value() == inv_alpha_out.has_value(),
               "out_snake: alpha_out and inv_alpha_out go together");
   if (alpha_out.has_value()) {
@@ -173,7 +173,7 @@ std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef 
     TORCH_CHECK(alpha_out->numel() == shape[1] && inv_alpha_out->numel() == shape[1],
                 "out_snake: one alpha per output channel");
   }
-  Tensor ys = alpha_out.has_value() ? empty_f(shape, like) : none_like(like);
+  Tensor ys = (alpha_out.has_value() && !no_ys) ? empty_f(shape, like) : none_like(like);
   Tensor y = (want_raw || !alpha_out.has_value()) ? empty_f(shape, like) : none_like(like);
   return {y, ys, Tensor()};
 }
@@ -182,6 +182,12 @@ float* opt_ptr(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 
 // Snake1d -> WNConv1d (+ residual, Tanh / Sigmoid, next Snake), models/layers.py:17-41, 52-89;
 // models/dac_vrvq.py:27-34, 62-74; models/importance_subnet.py:38-45.
+// snake(x) as three bf16 planes (B, 3, C / 8, T, 8) int16 (include/vrvq.h vrvq_conv1d_ex)
+Tensor planes_like(const Tensor& like, int64_t B, int64_t C, int64_t T) {
+  TORCH_CHECK(C % 8 == 0, "planes: channels must be a multiple of 8");
+  return at::empty({B, 3, C / 8, T, 8}, like.options().dtype(at::kShort));
+}
+
 std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed, int64_t cout,
                                         int64_t stride, int64_t pad, int64_t dil,
                                         const optional<Tensor>& bias,
@@ -190,35 +196,45 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
                                         const optional<Tensor>& residual, int64_t epilogue,
                                         const optional<Tensor>& alpha_out,
                                         const optional<Tensor>& inv_alpha_out, bool want_raw,
-                                        const optional<Tensor>& w_x3) {
-  check_t(x, "x");
+                                        const optional<Tensor>& w_x3, bool ys_planes) {
+  // x: (B, C, T) fp32, or snake(x) as planes (B, 3, C / 8, T, 8) int16 (the k7 planes tile)
+  const bool x_planes = x.scalar_type() == at::kShort;
+  check_t(x, "x", x_planes ? at::kShort : at::kFloat);
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
   check_opt(alpha, x, "alpha");
   check_opt(inv_alpha, x, "inv_alpha");
   check_opt(residual, x, "residual");
-  TORCH_CHECK(x.dim() == 3, "conv1d: x must be (B, C, T)");
-  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1),
-              "conv1d: w_packed must be (Cin, k, cout_pad) with Cin = x.shape[1]");
+  TORCH_CHECK(x_planes ? (x.dim() == 5 && x.size(1) == 3 && x.size(4) == 8) : x.dim() == 3,
+              "conv1d: x must be (B, C, T) fp32 or planes (B, 3, C/8, T, 8) int16");
+  const int64_t B = x.size(0);
+  const int64_t cin = x_planes ? x.size(2) * 8 : x.size(1);
+  const int64_t tin = x_planes ? x.size(3) : x.size(2);
+  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == cin,
+              "conv1d: w_packed must be (Cin, k, cout_pad) with Cin = x's channels");
   TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(), "conv1d: snake needs inv_alpha");
+  TORCH_CHECK(!ys_planes || alpha_out.has_value(), "conv1d: planes output needs out_snake");
   c10::DeviceGuard guard(x.device());
-  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
   const int64_t k = w_packed.size(1), cout_pad = w_packed.size(2);
   const int64_t tout = (tin + 2 * pad - dil * (k - 1) - 1) / stride + 1;
   TORCH_CHECK(tout > 0, "conv1d: input too short");
   if (residual.has_value())
     TORCH_CHECK(residual->sizes() == at::IntArrayRef({B, cout, tout}),
                 "conv1d: residual shape must equal the output shape");
-  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw, ys_planes);
+  if (ys_planes) ys = planes_like(x, B, cout, tout);
   // strided conv (k = 2 stride): w_x3 holds the planes of the phase-split weight (Cin * stride
   // view channels, 2 taps; include/vrvq.h vrvq_conv1d)
   const uint16_t* w3 = stride > 1 ? x3_ptr(w_x3, x, cin * stride, 2, cout_pad)
                                   : x3_ptr(w_x3, x, cin, k, cout_pad);
-  check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha), fp(inv_alpha),
-                       w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad, (int)k, (int)stride,
-                       (int)pad, (int)dil, fp(bias), fp(residual), (int)epilogue, opt_ptr(y),
-                       (int)tout, fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
-           "vrvq_conv1d");
+  check_rc(vrvq_conv1d_ex(x.data_ptr(), x_planes ? 1 : 0, (int)B, (int)cin, (int)tin, fp(alpha),
+                          fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad,
+                          (int)k, (int)stride, (int)pad, (int)dil, fp(bias), fp(residual),
+                          (int)epilogue, y.numel() ? y.data_ptr<float>() : nullptr, (int)tout,
+                          fp(alpha_out), fp(inv_alpha_out), ys_planes ? nullptr : opt_ptr(ys),
+                          ys_planes ? reinterpret_cast<uint16_t*>(ys.data_ptr<int16_t>()) : nullptr,
+                          stream_of(x)),
+           "vrvq_conv1d_ex");
   return {y, ys};
 }
 
@@ -257,7 +273,7 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
     const optional<Tensor>& bias, const optional<Tensor>& alpha,
     const optional<Tensor>& inv_alpha, const optional<Tensor>& alpha_out,
     const optional<Tensor>& inv_alpha_out, bool want_raw, int64_t pad,
-    const optional<Tensor>& w_x3) {
+    const optional<Tensor>& w_x3, bool ys_planes) {
   check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
@@ -274,14 +290,19 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
   c10::DeviceGuard guard(x.device());
   const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
   const int64_t tout = (tin - 1) * stride - 2 * p + 2 * stride;
-  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
+  TORCH_CHECK(!ys_planes || alpha_out.has_value(), "conv_transpose1d: planes output needs out_snake");
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw, ys_planes);
+  if (ys_planes) ys = planes_like(x, B, cout, tout);
   const uint16_t* w3 = x3_ptr(w_x3, x, cin, 2, w_packed.size(2));
-  check_rc(vrvq_conv_transpose1d_pad(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                                     fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
-                                     (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
-                                     opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
-                                     stream_of(x)),
-           "vrvq_conv_transpose1d_pad");
+  check_rc(vrvq_conv_transpose1d_ex(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                                    fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
+                                    (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
+                                    opt_ptr(y), fp(alpha_out), fp(inv_alpha_out),
+                                    ys_planes ? nullptr : opt_ptr(ys),
+                                    ys_planes ? reinterpret_cast<uint16_t*>(ys.data_ptr<int16_t>())
+                                              : nullptr,
+                                    stream_of(x)),
+           "vrvq_conv_transpose1d_ex");
   return {y, ys};
 }
 
@@ -1064,12 +1085,12 @@ TORCH_LIBRARY(vrvq, m) {
   m.def(
       "snake_conv1d(Tensor x, Tensor w_packed, int cout, int stride, int pad, int dil, "
       "Tensor? bias, Tensor? alpha, Tensor? inv_alpha, Tensor? residual, int epilogue, "
-      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw, Tensor? w_x3=None) -> "
-      "(Tensor, Tensor)");
+      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw, Tensor? w_x3=None, "
+      "bool ys_planes=False) -> (Tensor, Tensor)");
   m.def(
       "snake_conv_transpose1d(Tensor x, Tensor w_packed, int cout, int stride, Tensor? bias, "
       "Tensor? alpha, Tensor? inv_alpha, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw, int pad=-1, Tensor? w_x3=None) -> (Tensor, Tensor)");
+      "bool want_raw, int pad=-1, Tensor? w_x3=None, bool ys_planes=False) -> (Tensor, Tensor)");
   m.def(
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "

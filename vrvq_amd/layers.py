@@ -11,12 +11,21 @@ epilogue). Weight norm is folded once per parameter version, not per forward.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
 from . import ops
+
+
+# The residual units' k7 convs on the planes tile (csrc/conv_pl.h): their input snake(x) is
+# written as bf16 planes by the producing epilogue and staged by LDS-DMA. Off by default
+# (VRVQ_CONV_PLANES=1 turns it on): bit-identical, but slower over the step as measured --
+# the producers' planes epilogue costs more than the consumer saves (profiles/r05h_layers.txt:
+# 44.56 ms of convs vs 42.36 ms with fp32 snake(x) and the register-staged x3 tiles).
+PLANES = os.environ.get("VRVQ_CONV_PLANES", "0") == "1"
 
 
 def _param_key(*ps):
@@ -110,9 +119,12 @@ class WNConv1d(nn.Module):
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
                 residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE,
-                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True,
+                ys_planes: bool = False):
         """conv(snake(x)) (+ residual, epilogue). With out_snake (the consumer's Snake1d)
-        returns (y or None, out_snake(y)) computed in the same epilogue."""
+        returns (y or None, out_snake(y)) computed in the same epilogue; ys_planes: out_snake(y)
+        as bf16 planes for a planes k7 consumer. x may itself be such planes (snake(x) of a k7
+        conv, no snake here)."""
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
@@ -122,7 +134,7 @@ class WNConv1d(nn.Module):
                           bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                           residual=residual, epilogue=epilogue,
                           out_snake=None if out_snake is None else out_snake.prepared(),
-                          want_raw=want_raw, w_x3=self.prepared_x3())
+                          want_raw=want_raw, w_x3=self.prepared_x3(), ys_planes=ys_planes)
 
 
     def forward_fm(self, x: torch.Tensor, snake: Optional[Snake1d] = None) -> torch.Tensor:
@@ -182,7 +194,8 @@ class WNConvTranspose1d(nn.Module):
         return self._cache_x3[1]
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
-                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True,
+                ys_planes: bool = False):
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
@@ -191,7 +204,7 @@ class WNConvTranspose1d(nn.Module):
                                     bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                                     out_snake=None if out_snake is None else out_snake.prepared(),
                                     want_raw=want_raw, pad=self.padding[0],
-                                    w_x3=self.prepared_x3())
+                                    w_x3=self.prepared_x3(), ys_planes=ys_planes)
 
 
 class ResidualUnit(nn.Module):
@@ -218,7 +231,19 @@ class ResidualUnit(nn.Module):
             x = x[..., pad:-pad].contiguous()
         return self.block[3](y, snake=self.block[2], residual=x)
 
-    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool):
+    def runs_fused(self) -> bool:
+        C = self.block[1].in_channels
+        return self.fused and C in ops.RU_FUSED_CHANNELS and not (C == 256 and ops.X3 and
+                                                                 ops.RU256_SPLIT)
+
+    def takes_planes(self) -> bool:
+        """The chained form's k7 conv runs on the planes tile (its producer then writes
+        block[0](x) as planes): two launches, x3 weights, C a multiple of 64 from 128."""
+        C = self.block[1].in_channels
+        return PLANES and ops.X3 and not self.runs_fused() and C % 64 == 0 and C >= 128
+
+    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool,
+            out_planes: bool = False):
         """Chained form: x_snk = block[0](x) was produced by the previous layer's epilogue.
         For C in ops.RU_FUSED_CHANNELS one launch (vrvq_residual_unit: block[2](h) stays in
         LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
@@ -228,11 +253,10 @@ class ResidualUnit(nn.Module):
         fused set is C = 64 / 96 / 128 (and C = 256 without the x3 weights): C = 192 runs as two
         launches since the 192-row x3 k1 tiles (+2.8 % end to end,
         profiles/r04z_ru_fusion_ab.txt)."""
-        C = x.shape[1]
         # C = 256 with the x3 weights: the two launches (k7 on the x3 path at 128-row tiles,
         # then k1 + skip) beat the fused kernel, whose 256-row x3 weight stage does not fit
         # twice per CU and therefore keeps the fp32 MFMA (profiles/r02zi_bench_ab.txt)
-        if self.fused and C in ops.RU_FUSED_CHANNELS and not (C == 256 and ops.X3 and ops.RU256_SPLIT):
+        if self.runs_fused() and x_snk.dtype != torch.int16 and not out_planes:
             w7, cp7 = self.block[1].prepared()
             w1, cp1 = self.block[3].prepared()
             a2, ia2 = self.block[2].prepared()
@@ -242,11 +266,13 @@ class ResidualUnit(nn.Module):
                                      out_snake=out_snake.prepared(), want_raw=want_raw,
                                      w7_x3=self.block[1].prepared_x3(),
                                      w1_x3=self.block[3].prepared_x3())
-        return self.run_two_launch(x, x_snk, out_snake, want_raw)
+        return self.run_two_launch(x, x_snk, out_snake, want_raw, out_planes)
 
-    def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool):
+    def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool,
+                       out_planes: bool = False):
         _, h_snk = self.block[1](x_snk, out_snake=self.block[2], want_raw=False)
-        return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw)
+        return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw,
+                             ys_planes=out_planes)
 
 
 class EncoderBlock(nn.Module):
@@ -271,13 +297,18 @@ class EncoderBlock(nn.Module):
     def entry_snake(self) -> Snake1d:
         return self.block[0].block[0]
 
+    def takes_planes(self) -> bool:  # its first residual unit's k7 input
+        return self.block[0].takes_planes()
+
     def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Optional[Snake1d],
-            want_raw: bool):
-        """Chained form (see ResidualUnit.run); returns what block[4] returns."""
+            want_raw: bool, out_planes: bool = False):
+        """Chained form (see ResidualUnit.run); returns what block[4] returns. out_planes: the
+        consumer of out_snake(y) takes bf16 planes (the next block's first k7)."""
         for i in range(3):
             nxt = self.block[i + 1].block[0] if i < 2 else self.block[3]
-            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=i < 2)
-        return self.block[4](x_snk, out_snake=out_snake, want_raw=want_raw)
+            planes = i < 2 and self.block[i + 1].takes_planes()
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=i < 2, out_planes=planes)
+        return self.block[4](x_snk, out_snake=out_snake, want_raw=want_raw, ys_planes=out_planes)
 
 
 class DecoderBlock(nn.Module):
@@ -306,9 +337,12 @@ class DecoderBlock(nn.Module):
     def run(self, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool = False):
         """Chained form: x_snk = block[0](x) from the previous epilogue; returns
         (y or None, out_snake(y))."""
-        x, x_snk = self.block[1](x_snk, out_snake=self.block[2].block[0], want_raw=True)
+        x, x_snk = self.block[1](x_snk, out_snake=self.block[2].block[0], want_raw=True,
+                                 ys_planes=self.block[2].takes_planes())
         for i in range(2, 5):
             last = i == 4
             nxt = out_snake if last else self.block[i + 1].block[0]
-            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=want_raw if last else True)
+            planes = (not last) and self.block[i + 1].takes_planes()
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=want_raw if last else True,
+                                         out_planes=planes)
         return x, x_snk

@@ -62,7 +62,8 @@ class Encoder(nn.Module):
         for i in range(1, n - 2):
             last = i == n - 3
             nxt = None if last else self.block[i + 1].entry_snake()
-            r = self.block[i].run(x, x_snk, nxt, want_raw=True)
+            planes = (not last) and self.block[i + 1].takes_planes()
+            r = self.block[i].run(x, x_snk, nxt, want_raw=True, out_planes=planes)
             x, x_snk = (r, None) if last else r
         feat = x  # output of block index n-3 (the last EncoderBlock), models/dac_vrvq.py:43-44
         if frame_major:

@@ -99,19 +99,21 @@ def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k:
            alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
            out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, want_raw: bool = True,
-           w_x3: Optional[torch.Tensor] = None):
+           w_x3: Optional[torch.Tensor] = None, ys_planes: bool = False):
     """y = epi(residual + conv1d(snake(x)) + bias) on the MFMA implicit-GEMM kernel.
 
     out_snake = (alpha_next, inv_alpha_next) also produces snake_next(y) from the epilogue
     (the next layer's Snake). Returns y, or (y | None, snake_next(y)) when out_snake is given
     (y is None when want_raw is False). w_x3 = pack_x3_weight(w_packed, k) selects the bf16x3
-    split MFMA path for stride-1 convs (include/vrvq.h)."""
+    split MFMA path for stride-1 convs (include/vrvq.h). ys_planes: snake_next(y) comes back as
+    bf16 planes (B, 3, Cout/8, T, 8) int16, the input layout of the k7 planes tile; x may be such
+    a planes tensor (snake(x) for a k7 conv, alpha None: include/vrvq.h vrvq_conv1d_ex)."""
     if w_packed.dim() != 3 or w_packed.shape[1] != k or w_packed.shape[2] != cout_pad:
         raise RuntimeError("conv1d: w_packed must be (Cin, k, cout_pad)")
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv1d(x, w_packed, int(cout), int(stride), int(pad), int(dil), bias,
                                 alpha, inv_alpha, residual, int(epilogue), ao, io, bool(want_raw),
-                                w_x3)
+                                w_x3, bool(ys_planes))
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -133,12 +135,13 @@ def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pa
                      inv_alpha: Optional[torch.Tensor] = None,
                      out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                      want_raw: bool = True, pad: int = -1,
-                     w_x3: Optional[torch.Tensor] = None):
+                     w_x3: Optional[torch.Tensor] = None, ys_planes: bool = False):
     """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d. pad -1 is
     the DecoderBlock's ceil(stride / 2), 0 the padding=False window of the chunked codec."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv_transpose1d(x, w_packed, int(cout), int(stride), bias, alpha,
-                                          inv_alpha, ao, io, bool(want_raw), int(pad), w_x3)
+                                          inv_alpha, ao, io, bool(want_raw), int(pad), w_x3,
+                                          bool(ys_planes))
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -390,18 +393,25 @@ def _register_fakes():
         y = f32(x, shape) if (want_raw or ao is None) else none(x)
         return y, ys
 
+    def planes(x, B, C, T):
+        return x.new_empty((B, 3, C // 8, T, 8), dtype=torch.int16)
+
     @reg("vrvq::snake_conv1d")
     def _(x, w_packed, cout, stride, pad, dil, bias, alpha, inv_alpha, residual, epilogue,
-          alpha_out, inv_alpha_out, want_raw, w_x3=None):
-        B, _c, tin = x.shape
+          alpha_out, inv_alpha_out, want_raw, w_x3=None, ys_planes=False):
+        B = x.shape[0]
+        tin = x.shape[3] if x.dim() == 5 else x.shape[2]
         tout = conv_out_len(tin, w_packed.shape[1], stride, pad, dil)
-        return pair(x, (B, cout, tout), alpha_out, want_raw)
+        y, ys = pair(x.new_empty((1,), dtype=torch.float32), (B, cout, tout), alpha_out, want_raw)
+        return y, planes(x, B, cout, tout) if ys_planes else ys
 
     @reg("vrvq::snake_conv_transpose1d")
     def _(x, w_packed, cout, stride, bias, alpha, inv_alpha, alpha_out, inv_alpha_out, want_raw,
-          pad=-1, w_x3=None):
+          pad=-1, w_x3=None, ys_planes=False):
         B, _c, tin = x.shape
-        return pair(x, (B, cout, convt_out_len(tin, stride, pad)), alpha_out, want_raw)
+        tout = convt_out_len(tin, stride, pad)
+        y, ys = pair(x, (B, cout, tout), alpha_out, want_raw)
+        return y, planes(x, B, cout, tout) if ys_planes else ys
 
     @reg("vrvq::residual_unit")
     def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw,
