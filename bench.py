@@ -48,7 +48,9 @@ X3_PEAK_TFLOPS = 2516.6 / 6    # fp32 FLOPs on the bf16 MFMA with the exact 3-wa
 CLIP_SAMPLES = 44100
 SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
-RVQ_KERNELS = ("rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
+# the reference inference driver's own sweep (scripts/inference.py:58-70: 10-s clips, 12 levels)
+LEVELS_INFERENCE = (0.2, 0.3, 0.4, 0.5, 0.6, 0.8, 1.0, 1.2, 1.5, 2.0, 2.5, 3.0)
+RVQ_KERNELS = ("rvq_fm_kernel", "rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
                "rvq_chain_kernel", "rvq_expand_kernel")
 
 
@@ -170,18 +172,22 @@ class RvqTimer:
 
     def install(self):
         from vrvq_amd import ops
-        orig = ops.rvq_encode
 
-        def timed(*a, **k):
-            if not self.enabled:
-                return orig(*a, **k)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(torch.cuda.current_stream())
-            r = orig(*a, **k)
-            e1.record(torch.cuda.current_stream())
-            self.events.append((e0, e1))
-            return r
-        ops.rvq_encode = timed
+        def wrap(orig):
+            def timed(*a, **k):
+                if not self.enabled:
+                    return orig(*a, **k)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(torch.cuda.current_stream())
+                r = orig(*a, **k)
+                e1.record(torch.cuda.current_stream())
+                self.events.append((e0, e1))
+                return r
+            return timed
+        # the channel-major entry and the frame-major one the eval encode takes (model.py RVQ_FM)
+        ops.rvq_encode = wrap(ops.rvq_encode)
+        ops.rvq_encode_fm = wrap(ops.rvq_encode_fm)
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -338,6 +344,14 @@ def main(argv=None):
     ap.add_argument("--n-codebooks", type=int, default=8)
     ap.add_argument("--level", type=float, default=1.0)
     ap.add_argument("--sweep", action="store_true", help="configs[4]: VBR level sweep")
+    ap.add_argument("--clip-seconds", type=float, default=1.0,
+                    help="clip length (1 s: configs[1..4]; 10 with --batch 1 --sweep: the "
+                         "reference inference driver's shape, scripts/inference.py:58-70)")
+    ap.add_argument("--levels", default=None,
+                    help="sweep levels, comma separated (default: configs[4]'s 0.25,0.5,1,2 for "
+                         "1-s clips, inference.py:69's 12 levels for longer clips)")
+    ap.add_argument("--max-decode-clips", type=int, default=None,
+                    help="sweep: decode the levels' z_q in batches of at most this many clips")
     ap.add_argument("--train", action="store_true",
                     help="configs[3]: vrvq_a2 training step (generator + discriminator + losses, "
                          "DDP over RCCL), 0.38 s clips")
@@ -349,6 +363,11 @@ def main(argv=None):
     args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 16 if args.sweep else 32
+    clip = int(round(args.clip_seconds * SR))
+    if args.levels:
+        levels = tuple(float(v) for v in args.levels.split(","))
+    else:
+        levels = LEVELS if clip == CLIP_SAMPLES else LEVELS_INFERENCE
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `python bench.py --gpus N` without a launcher: start the N ranks ourselves. Nothing
@@ -377,7 +396,7 @@ def main(argv=None):
         return
 
     model, kwargs = build_model(args, dev)
-    audio = torch.from_numpy(synthetic_audio(args.batch, CLIP_SAMPLES,
+    audio = torch.from_numpy(synthetic_audio(args.batch, clip,
                                              seed=shard_seed(1234, rank))).to(dev)
     timer = RvqTimer()
     timer.install()
@@ -398,15 +417,17 @@ def main(argv=None):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-                masks, z_all = sweep_latents(enc["imp_map"], enc["z_q_is"], LEVELS, nq)
-                y = model.decode(z_all)
+                masks, z_all = sweep_latents(enc["imp_map"], enc["z_q_is"], levels, nq)
+                cap = args.max_decode_clips or z_all.shape[0]
+                y = torch.cat([model.decode(z_all[i:i + cap])
+                               for i in range(0, z_all.shape[0], cap)])
                 bpfs = [vrvq_amd.ops.bpf(m, bits) for m in masks]
                 e1.record()
                 if timer.enabled:
                     lvl_ev["all"].append((e0, e1))
                 B = args.batch
                 return [(lv, masks[i], bpfs[i], y[i * B:(i + 1) * B])
-                        for i, lv in enumerate(LEVELS)]
+                        for i, lv in enumerate(levels)]
     else:
         def step():
             with torch.no_grad():
@@ -421,8 +442,8 @@ def main(argv=None):
     res_t = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize, device=dev,
                         on_start=on, on_stop=off)
     ms_per_step = res_t.seconds / args.steps * 1e3
-    value = throughput(args.batch * CLIP_SAMPLES / SR, res_t)
-    T = math.ceil(CLIP_SAMPLES / model.hop_length)
+    value = throughput(args.batch * clip / SR, res_t)
+    T = math.ceil(clip / model.hop_length)
     rvq_ms = timer.mean_ms()
     kern_ms, kern_n, per_call = timer.kernel_ms()
     byt = rvq_bytes(args.batch, T, nq)
@@ -431,32 +452,35 @@ def main(argv=None):
     # events there)
     dur_ms = kern_ms * per_call if kern_n else rvq_ms
     achieved = byt / (dur_ms * 1e-3) / 1e9
-    fl_enc, fl_dec = conv_flops(model, args.batch, 44544)
-    flops = fl_enc + (len(LEVELS) if args.sweep else 1) * fl_dec
+    fl_enc, fl_dec = conv_flops(model, args.batch, T * model.hop_length)
+    flops = fl_enc + (len(levels) if args.sweep else 1) * fl_dec
     levels_rep = None
     if args.sweep:
         levels_rep = []
         ms = float(np.mean([a.elapsed_time(b) for a, b in lvl_ev["all"]]))
         for lv, mask, bpf_t, _y in res_t.last:
-            rep = job_rate(args.batch * CLIP_SAMPLES / SR, float((mask.double() * 10.0).sum()),
+            rep = job_rate(args.batch * clip / SR, float((mask.double() * 10.0).sum()),
                            mask.shape[0] * mask.shape[2], fps, device=dev)
             levels_rep.append({"level": lv, "bpf": round(rep.bpf, 6), "kbps": round(rep.kbps, 4),
                                "bpf_rank0_kernel": round(float(bpf_t), 6),
                                "decode_ms_all_levels_rank0": round(ms, 3),
                                "decode_audio_sec_per_s_all_levels": round(
-                                   len(LEVELS) * rep.audio_seconds / (ms * 1e-3), 2)})
+                                   len(levels) * rep.audio_seconds / (ms * 1e-3), 2)})
     conv_ms = ms_per_step - rvq_ms
     conv_tflops = flops / (conv_ms * 1e-3) / 1e12
-    shape = {(32, 8): False, (64, 32): True}.get((args.batch, nq)) if not args.sweep else None
+    shape = ({(32, 8): False, (64, 32): True}.get((args.batch, nq))
+             if not args.sweep and clip == CLIP_SAMPLES else None)
     traffic, traffic_src = rvq_pmc_traffic(shape) if shape is not None else (None, None)
     split, split_src = rvq_kernel_split(shape) if shape is not None else (None, None)
     ranks_seen = int(sum_over_ranks([1.0], dev)[0])
     if rank == 0:
-        workload = ("DAC_VRVQ conf/base.yml VBR, level sweep {0.25,0.5,1,2}: encode once + per "
-                    "level mask/masked-sum/decode/bpf (scripts/inference.py:88-112)"
+        lv_txt = ",".join(f"{v:g}" for v in levels)
+        workload = (f"DAC_VRVQ conf/base.yml VBR, {args.clip_seconds:g}-s clips, level sweep "
+                    f"{{{lv_txt}}}: encode once + per level mask/masked-sum/decode/bpf "
+                    "(scripts/inference.py:88-112)"
                     if args.sweep else
-                    f"DAC_VRVQ VBR {nq} cb, level {args.level}, preprocess+encode+decode "
-                    "(z_q_is materialised)")
+                    f"DAC_VRVQ VBR {nq} cb, level {args.level}, {args.clip_seconds:g}-s clips, "
+                    "preprocess+encode+decode (z_q_is materialised)")
         res = {
             "metric": "audio-sec/s encode+RVQ+decode, 44.1 kHz batch-32, 1->8 MI355X; RVQ HBM GB/s",
             "value": round(value, 3),
@@ -472,15 +496,16 @@ def main(argv=None):
             "dtype": "f32",
             "data": "synthetic uniform audio [-0.5,0.5), recipe random-init weights",
             "config": {"workload": workload, "model": f"DAC_VRVQ base ({nq} cb)",
-                       "global_batch": args.batch * world, "clip_samples": CLIP_SAMPLES,
+                       "global_batch": args.batch * world, "clip_samples": clip,
                        "n_codebooks": nq,
                        "parallelism": f"dp{world} (replicas, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "RVQ path: one torch.ops.vrvq.rvq_encode = rvq_fused_kernel, "
-                                   "one launch per <= 32 clips at T <= 96 (projection units "
-                                   "-> chain parts -> expansion workgroups, in-launch tagged-"
+                         "kernel": "RVQ path: one torch.ops.vrvq.rvq_encode_fm = rvq_fm_kernel, "
+                                   "one launch per <= 32 clips (chain parts project their own "
+                                   "frames of the encoder's frame-major z, then the stage chain; "
+                                   "expansion workgroups write z_q_is / z_q; in-launch tagged-"
                                    "granule hand-offs)",
                          "bytes_per_call": byt,
                          "kernel_us": round(kern_ms * 1e3, 2) if kern_n else None,

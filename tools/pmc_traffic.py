@@ -5,12 +5,11 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters). Per
 MI355X_MICROARCH.md (HBM / rocprofv3), gfx950's FETCH_SIZE reports exactly half of the bytes of
 a wide coalesced streaming read, so the fetch bytes are doubled; WRITE_SIZE is exact for
-16-B-per-lane streaming stores (the expansion's stores are 4-B-per-lane rows: uncalibrated,
-reported as read).
+16-B-per-lane streaming stores (the expansion's z_q_is / z_q stores are 16 B per lane).
 
     python tools/pmc_traffic.py gpurun_out/<tag> profiles/<tag>_rvq_pmc.json [launches per call]
 
-The path is rvq_fused_kernel where the fused launch ran (one dispatch per <= 32 clips: the
+The path is rvq_fm_kernel (the frame-major launch) or rvq_fused_kernel where a fused launch ran (one dispatch per <= 32 clips: the
 third argument, default 1, scales a dispatch to one rvq_encode call), else the three kernels.
 """
 import collections
@@ -42,7 +41,9 @@ def main():
         kernels[k] = {"fetch_size_kib": f_kib, "write_size_kib": w_kib,
                       "fetch_bytes_corrected": 2 * f_kib * 1024, "write_bytes": w_kib * 1024,
                       "total": 2 * f_kib * 1024 + w_kib * 1024}
-    if "rvq_fused_kernel" in kernels:
+    if "rvq_fm_kernel" in kernels:
+        path = ["rvq_fm_kernel"]
+    elif "rvq_fused_kernel" in kernels:
         path = ["rvq_fused_kernel"]
     else:
         path = [k for k in kernels

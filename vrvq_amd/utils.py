@@ -68,20 +68,28 @@ def sweep_latents(imp_map: torch.Tensor, z_q_is: torch.Tensor, levels: Sequence[
 
 
 def level_sweep(model, audio: torch.Tensor, levels: Sequence[float], bits_per_codebook: int = 10,
-                decode: bool = True):
+                decode: bool = True, max_decode_clips: int | None = None):
     """The reference's VBR level sweep (scripts/inference.py:88-112) without file I/O.
 
     Encodes once (level 1), then for each level: hard mask of imp_map * (level * Nq),
-    masked sum of z_q_is, bpf and kbps. The levels' z_q go through ONE decode of L*B clips
-    (the reference decodes level by level; clips are independent and the decoder is batch
-    invariant, so the per-level outputs are the same — tests/test_gpu_parity.py checks the
-    batched recon against the reference's per-level fixtures). Returns a list of dicts."""
+    masked sum of z_q_is, bpf and kbps. The levels' z_q are decoded as batches of up to
+    `max_decode_clips` clips (default: all L*B at once, the fastest; the reference decodes level
+    by level, so a cap of B keeps its peak decoder memory). Clips are independent, but a conv's
+    tile choice can depend on the batch size, so the per-level recon agrees with a per-level
+    decode within fp32 rounding, not bit for bit (tests/test_gpu_parity.py checks the batched
+    recon against the reference's per-level fixtures). Returns a list of dicts."""
     n_q = model.n_codebooks
     with torch.no_grad():
         x = model.preprocess(audio, model.sample_rate)
         enc = model.encode(x, n_quantizers=None, level=1)
         masks, z_all = sweep_latents(enc["imp_map"], enc["z_q_is"], levels, n_q)
-        recon_all = model.decode(z_all) if decode else None
+        recon_all = None
+        if decode:
+            cap = max_decode_clips or z_all.shape[0]
+            if cap < 1:
+                raise ValueError("max_decode_clips must be >= 1")
+            recon_all = torch.cat([model.decode(z_all[i:i + cap])
+                                   for i in range(0, z_all.shape[0], cap)])
     B = audio.shape[0]
     out = []
     for li, level in enumerate(levels):
