@@ -31,11 +31,14 @@ def _fm_call(z, st, imp, level, zqis=True):
     (28, 1024, 2, 70, True), (8, 1024, 3, 96, True), (8, 1024, 2, 97, True),
     (8, 1024, 2, 128, True), (8, 1024, 2, 129, False), (8, 1024, 2, 200, True),
     (32, 1024, 2, 120, True), (9, 1024, 2, 87, True), (5, 1024, 3, 40, False),
-    (12, 1024, 1, 862, True)])
+    (12, 1024, 1, 862, True), (8, 1024, 2, 66, True), (8, 1024, 2, 101, True),
+    (8, 1024, 2, 94, False), (8, 1024, 2, 3, True), (8, 1024, 2, 35, True)])
 def test_rvq_fm_vs_fp64(nq, ncode, B, T, vbr):
     """Every codebook size (N/256 = 1..4), nq 1..32 (odd, > 8), one frame, partial parts,
     T > 96 / 128 (several expansion frame blocks, 16-frame parts; nq = 32 at T = 120 on smaller
-    parts to fit the LDS) and a 10-s clip (T = 862): codes / masks exact vs fp64, z_q_is / z_q
+    parts to fit the LDS), a 10-s clip (T = 862) and every kind of ragged last quad (T % 4 =
+    1..3 inside a frame tile: one shifted 16-B store; at a tile's first quad or T < 4: elementwise
+    stores): codes / masks exact vs fp64, z_q_is / z_q
     within 1e-5; z_q is the op's own masked sum of z_q_is bit for bit."""
     q, gen = _random_rvq(nq, ncode, 1000 * nq + T + 7)
     st = q.stacked()

@@ -591,6 +591,12 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     // per CU, otherwise three 32-wide tiles (more workgroups for the deep-K, narrow-N GEMMs).
     const long long blocks96 = (long long)((a.M + 127) / 128) * batch;
     bn = blocks96 >= conv_bn96_min() ? 96 : 32;
+    // 2-tap x3 GEMMs: the 32-wide tile pairs its K octets (conv_x3.h x3_pair) and the 96-wide
+    // one does not, so a clip's sums would change order with the batch. Their width is fixed
+    // instead (batch-invariant outputs, tests/test_gpu_parity.py test_batch_invariance_*): the
+    // polyphase ConvTranspose (up > 0) 96-wide, the phase-split strided convs 32-wide -- what
+    // configs[1] (B = 32) ran before.
+    if (KS == 2 && a.w3 != nullptr) bn = a.up > 0 ? 96 : 32;
   }
   // k = 16 (the stride-8 encoder convs): the 8 MB weight block does not fit in L2, so the
   // 128-wide tile's halved weight re-streaming beats its padding (1490 -> 1323 us at T = 696,

@@ -1246,7 +1246,11 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   unsigned nact[2];  // per output frame u: the number of active stages (mask = i < n), bytes
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int tb = fb * FU_FB + (ft0 + 2 * j) * 32;  // the tile's first frame
+    // the tile's first frame; a clip's last, partial tile is moved back to end at the clip's
+    // last frame (it overlaps the tile before it: those frames are computed and written twice,
+    // with identical values), so every quad of four frames is whole from T = 32 on
+    int tb = fb * FU_FB + (ft0 + 2 * j) * 32;
+    if (tb + 32 > T && T >= 32) tb = T - 32;
     const int tc = min(tb + col, T - 1);
     const int p = tc / F, fr = tc - p * F;
     zoff[j] = ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
@@ -1298,7 +1302,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
     return __builtin_amdgcn_ballot_w64(!good) == 0;
   };
   // four consecutive frames of one channel: one 16-B store (rows of T floats are dword-
-  // aligned), elementwise at the clip's last, partial quad
+  // aligned); elementwise only where a clip is shorter than a frame tile (T < 32)
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
   auto store_quad = [&](float* row, int t, float v0, float v1, float v2, float v3) {
     if (t + 4 <= T) {
