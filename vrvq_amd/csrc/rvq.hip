@@ -1181,21 +1181,22 @@ struct FusedArgs {
 // instruction (r04's 4-B stores needed 4x the instructions; 16-B stores straight from the
 // frame-major D orientation touched 32 rows per instruction and ran slower still:
 // profiles/r05i_stamps.log). Bias and mask are then per register (the three-launch kernel's
-// expressions, per element). Every wave runs on its own (no barrier). The stage's zst rows are
-// tagged granules (the chain's S2 stores): a wave loads stage i + 1's granules (and its
-// W_out row / biases) speculatively BEFORE stage i's stores and checks their tags when it gets
-// there -- vmcnt retires in order, so a load issued after the stores would wait for them to
-// drain (profiles/r04d_fused_timeline.txt). Rows whose tags are not this call's stage yet are
-// re-read until they are (bounded; on the bound the tile's outputs are NaN).
-// What bounds a stage is the z_q_is write stream (11.4 MB per stage at B = 32, ~4 us: ~2.9 TB/s
-// next to the chain's traffic); without z_q_is the expansion keeps pace with the chain
-// (profiles/r05j_stamps_nozqis.log), and unconditional buffer stores -- so that no load ever
-// waits for the stores to drain -- changed nothing (profiles/r05l_stamps_unconditional_stores.log).
+// expressions, per element).
+// The stage's zst rows are tagged granules (the chain's S2 stores). The workgroup reads its
+// 128-frame window of them ONCE per stage, 16 B per lane, into an LDS slab (double-buffered,
+// one barrier per stage) that every wave takes its B operands from -- r05k's waves each read
+// the rows of their own tiles, 4x the workgroup's sc1 reads. A lane loads its slice of stage
+// i + 1 (and its W_out row / biases) speculatively BEFORE stage i's stores and checks the tags
+// when it gets there -- vmcnt retires in order, so a load issued after the stores would wait
+// for them to drain (profiles/r04d_fused_timeline.txt). Slices whose tags are not this call's
+// stage yet are re-read until they are (bounded; on the bound the outputs are NaN).
+// What bounds a stage is the z_q_is write stream (11.4 MB per stage at B = 32); the same store
+// pattern alone writes at 4-5.7 TB/s (tools/micro/expand_writes.hip), next to the chain ~2.7.
 struct ExOps {
   float4 w0, w1;
   float bb[4];    // b_out of the lane's four output channels (one per register quad)
-  u32x4 z[2][2];  // per frame tile: 4 granules {zst k = 2 s + h, tag}, s = 0..3
 };
+constexpr int FU_EX_LDS = 2 * FU_FB * RCD * 4;  // the zst slab, two stages
 
 // 4 x 4 transpose inside each lane quad: lane 4 g + k, register 4 qd + u holds E(u, k) on
 // entry and E(k, u) on exit (E(row, column) of the quad's 4 x 4 block). Two butterfly steps,
@@ -1222,14 +1223,14 @@ __device__ __forceinline__ void quad_transpose(f32x16& q, int lane) {
 }
 
 __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, float* sm) {
-  (void)sm;
   const int nq = f.c.nq, T = f.c.T, F = f.c.F;
   constexpr int NCB = RD / FU_CB;
   const int cb = e % NCB;
   const int fb = (e / NCB) % f.n_fb;
   const int b = e / (NCB * f.n_fb);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = cb * FU_CB + (wave & 3) * 32;
   const int col = lane & 31, h = lane >> 5;
   const int n_ft = (min(FU_FB, T - fb * FU_FB) + 31) / 32;  // frame tiles of this block
@@ -1241,7 +1242,18 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   // after the transpose: lane (g = col >> 2, k = lane & 3, h), register 4 qd + u holds channel
   // c0 + 8 qd + 4 h + k, frame tile_base + 4 g + u
   const int chk = c0 + 4 * h + (lane & 3);  // + 8 qd
-  int zoff[2];    // byte offset of this lane's 4 granules of stage 0 (its B-operand frame col)
+  // the slab window: 128 frames from wlo (the last block's window ends at the clip's last frame,
+  // so it holds the moved-back last tile); lane tid loads frame wlo + (tid >> 2), dims
+  // 2 (tid & 3) + {0, 1} (frames past the clip re-read its last one: loaded, never used)
+  const int wlo = T >= FU_FB ? min(fb * FU_FB, T - FU_FB) : 0;
+  const int fi = tid >> 2, dp = tid & 3;
+  int soff;
+  {
+    const int t = min(wlo + fi, T - 1);
+    const int p = t / F, fr = t - p * F;
+    soff = ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 2 * dp) * 8;
+  }
+  int trow[2];    // the lane's B-operand frame (col) as a slab row
   int tq[2];      // first of the lane's four output frames
   unsigned nact[2];  // per output frame u: the number of active stages (mask = i < n), bytes
 #pragma unroll
@@ -1251,9 +1263,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
     // with identical values), so every quad of four frames is whole from T = 32 on
     int tb = fb * FU_FB + (ft0 + 2 * j) * 32;
     if (tb + 32 > T && T >= 32) tb = T - 32;
-    const int tc = min(tb + col, T - 1);
-    const int p = tc / F, fr = tc - p * F;
-    zoff[j] = ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 4 * h) * 8;
+    trow[j] = min(tb - wlo + col, FU_FB - 1);
     tq[j] = tb + 4 * (col >> 2);
     float sv[4];  // the loads first: one memory latency
 #pragma unroll
@@ -1276,30 +1286,18 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   const float* wp = f.w_out + (size_t)(c0 + col) * RCD;  // A operand: channel row c0 + col
   const size_t wstride = (size_t)RD * RCD;
   const unsigned base = f.epoch * 64u;
-  auto load_z = [&](int i, u32x4 (&z)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int off = zoff[j] + i * zstage;
-      z[j][0] = __builtin_amdgcn_raw_buffer_load_b128(zr, off, 0, CPOL_SC1);
-      z[j][1] = __builtin_amdgcn_raw_buffer_load_b128(zr, off + 16, 0, CPOL_SC1);
-    }
+  auto load_s = [&](int i) {
+    return __builtin_amdgcn_raw_buffer_load_b128(zr, soff + i * zstage, 0, CPOL_SC1);
   };
   auto load = [&](int i, ExOps& o) {
     o.w0 = ld4(wp + i * wstride);
     o.w1 = ld4(wp + i * wstride + 4);
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) o.bb[qd] = f.b_out[(size_t)i * RD + chk + 8 * qd];
-    load_z(i, o.z);
   };
-  auto tagged = [&](const u32x4 (&z)[2][2], int i) -> bool {  // wave-uniform
+  auto late = [&](const u32x4& g, int i) -> bool {  // wave-uniform: a slice is not stage i's
     const unsigned tag = base + (unsigned)i + 1u;
-    bool good = true;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      if (j == 0 ? one : two)
-        good = good && z[j][0][1] == tag && z[j][0][3] == tag && z[j][1][1] == tag &&
-               z[j][1][3] == tag;
-    return __builtin_amdgcn_ballot_w64(!good) == 0;
+    return __builtin_amdgcn_ballot_w64(!(g[1] == tag && g[3] == tag)) != 0;
   };
   // four consecutive frames of one channel: one 16-B store (rows of T floats are dword-
   // aligned); elementwise only where a clip is shorter than a frame tile (T < 32)
@@ -1318,40 +1316,37 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) zq[j][r] = 0.0f;
-  ExOps cur;
-  __shared__ int xdead_s;  // wave 0's stage-0 wait ran out (then no wave waits any more)
-  bool dead = false;       // a wait ran out: no more waits (err recorded), outputs NaN
-  // stage 0 lands after the chain's first stage: wave 0 alone watches its rows with a long
-  // sleep between looks, the others wait at the barrier
-  if (wave == 0) {
-    for (unsigned it = 0;; ++it) {
-      load_z(0, cur.z);
-      if (tagged(cur.z, 0)) break;
-      if (it >= f.spin_max) {
-        if (lane == 0) report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
-        dead = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(16);
-    }
-    if (lane == 0) xdead_s = dead ? 1 : 0;
-  }
+  __shared__ int xdead_s;  // some wave's wait ran out (then no wave waits any more)
+  if (tid == 0) xdead_s = 0;
   __syncthreads();
-  dead = xdead_s != 0;
+  bool dead = false;       // a wait ran out: no more waits (err recorded), outputs NaN
+  u32x4 g = load_s(0);
+  ExOps cur;
   load(0, cur);
   for (int i = 0; i < nq; ++i) {
-    for (unsigned it = 0; !dead && !tagged(cur.z, i); ++it) {
-      if (it >= f.spin_max) {
-        if (lane == 0) report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
-        dead = true;
-        break;
+    if (!dead && late(g, i)) {
+      // stage 0 lands after the chain's first stage: long sleeps between looks
+      for (unsigned it = 0;; ++it) {
+        if (it >= f.spin_max) {
+          if (lane == 0) report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
+          xdead_s = 1;
+          dead = true;
+          break;
+        }
+        if (i == 0) __builtin_amdgcn_s_sleep(16); else __builtin_amdgcn_s_sleep(4);
+        g = load_s(i);
+        if (!late(g, i)) break;
       }
-      __builtin_amdgcn_s_sleep(4);
-      load_z(i, cur.z);
     }
+    float* slab = sm + (i & 1) * (FU_FB * RCD);
+    *reinterpret_cast<float2*>(slab + fi * RCD + 2 * dp) =
+        make_float2(__uint_as_float(g[0]), __uint_as_float(g[2]));
+    __syncthreads();  // the stage's slab is whole; the other buffer is free (stage i - 1 done)
+    dead = xdead_s != 0;
     FSTAMP(f.stamps, 1 + i);
     // the next stage's operands ahead of this stage's stores (unconditional, clamped stage: a
     // branch around loads makes the waitcnt pass drain at the join)
+    g = load_s(min(i + 1, nq - 1));
     ExOps nxt;
     load(min(i + 1, nq - 1), nxt);
     const float wa[4] = {h ? cur.w0.y : cur.w0.x, h ? cur.w0.w : cur.w0.z,
@@ -1359,17 +1354,17 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (!(j == 0 ? one : two)) break;
-      const float zb[4] = {__uint_as_float(cur.z[j][0][0]), __uint_as_float(cur.z[j][0][2]),
-                           __uint_as_float(cur.z[j][1][0]), __uint_as_float(cur.z[j][1][2])};
+      const float4 zb = *reinterpret_cast<const float4*>(slab + trow[j] * RCD + 4 * h);
       f32x16 q;
 #pragma unroll
       for (int r = 0; r < 16; ++r) q[r] = 0.0f;
 #ifdef VRVQ_STAMPS
       if (!(f.dbg & 1)) {
 #endif
-#pragma unroll
-      for (int st = 0; st < 4; ++st)
-        q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[st], zb[st], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[0], zb.x, q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[1], zb.y, q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[2], zb.z, q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[3], zb.w, q, 0, 0, 0);
 #ifdef VRVQ_STAMPS
       }
 #endif
@@ -1476,6 +1471,7 @@ __host__ __device__ inline int fm_ksplit(int nq) {  // K parts per row tile
 }
 // LDS of rvq_fm_kernel: the chain carve, overlaid by the K-half planes during the projection,
 // then the S - 1 partial tiles of the K split
+static_assert(LP_LDS >= FU_EX_LDS, "the expansion's zst slab fits the projection's LDS");
 __host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
   size_t c = (size_t)ChainLds(nq, F, N).total * sizeof(float);
   if (c < (size_t)LP_LDS) c = LP_LDS;
@@ -1962,6 +1958,7 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
   size_t lds = (size_t)ChainLds(nq, F, 256 * NM).total * sizeof(float);
   const size_t lds_pj = PJ3 ? (size_t)PJ3_LDS : (size_t)PJ_CPS * PJ2_LD * sizeof(float);
   if (lds < lds_pj) lds = lds_pj;
+  if (lds < (size_t)FU_EX_LDS) lds = FU_EX_LDS;
   if (lds > 80 * 1024) return FUSED_NA;
   const void* kern = (const void*)rvq_fused_kernel<NM, PJ3>;
   const int cap = min(FU_CLIPS_MAX, fused_clip_capacity(kern, lds, 2 * FU_NP));
