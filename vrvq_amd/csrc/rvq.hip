@@ -1482,18 +1482,31 @@ __host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
 // NKS consecutive k-steps (32 channels each) of one 16-row tile against the staged K-half:
 // the A planes come from L2 in a ring three k-steps deep (36 VGPRs in flight per lane), each
 // k-step's six products in the x3 order m m, h l, l h, h m, m h, h h.
+constexpr int FM_DEPTH = 3, FM_PRIME = 1;  // ring depth; k-steps primed under the z loads
+template <int NKS>
+__device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
+                                         u32x4 (&a)[FM_DEPTH][3], int j0 = 0,
+                                         int j1 = FM_PRIME) {
+  constexpr int DEPTH = NKS < FM_DEPTH ? NKS : FM_DEPTH;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < DEPTH; ++j)
+    if (j >= j0 && j < j1)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[j][p] = w3[((size_t)((ks0 + j) * 3 + p) * n_rt + rt) * 64 + lane];
+}
+// (primed: the ring's first DEPTH k-steps are already in flight in `a`, fm_prime)
 template <int NKS>
 __device__ __forceinline__ void fm_ksteps(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
-                                          int h, const char* lds, f32x4& acc) {
-  constexpr int DEPTH = NKS < 3 ? NKS : 3;
+                                          int h, const char* lds, f32x4& acc,
+                                          u32x4 (&a)[FM_DEPTH][3], bool primed) {
+  constexpr int DEPTH = NKS < FM_DEPTH ? NKS : FM_DEPTH;
   const int lane = threadIdx.x & 63, lr = lane & 15, kg = lane >> 4;
-  u32x4 a[DEPTH][3];
   auto load_a = [&](int j, u32x4 (&dst)[3]) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) dst[p] = w3[((size_t)((ks0 + j) * 3 + p) * n_rt + rt) * 64 + lane];
   };
-#pragma unroll
-  for (int j = 0; j < DEPTH; ++j) load_a(j, a[j]);
+  fm_prime<NKS>(w3, n_rt, rt, ks0, a, primed ? FM_PRIME : 0, FM_DEPTH);
 #pragma unroll
   for (int j = 0; j < NKS; ++j) {
     const int kk = (ks0 + j - 16 * h) * 32 + 8 * kg;  // channel within the half
@@ -1549,6 +1562,17 @@ __device__ __forceinline__ void project_fm_body(const FusedArgs& f, int b, int t
     const bool act = it < n_items;  // wave-uniform
     const int rt = min(it, n_items - 1) / S, kq = min(it, n_items - 1) % S;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // half 0's first k-steps of W_in in flight under the z loads and the slab's staging
+    u32x4 ring[FM_DEPTH][3];
+    {
+      const int ks0 = kq * (16 / S);
+      switch (S) {
+        case 1: fm_prime<16>(w3, n_rt, rt, ks0, ring); break;
+        case 2: fm_prime<8>(w3, n_rt, rt, ks0, ring); break;
+        case 4: fm_prime<4>(w3, n_rt, rt, ks0, ring); break;
+        default: fm_prime<2>(w3, n_rt, rt, ks0, ring); break;
+      }
+    }
     for (int h = 0; h < 2; ++h) {
       // stage K-half h (every item round: nq >= 16 runs more than one round)
       __syncthreads();  // the previous half's planes are no longer read
@@ -1569,11 +1593,12 @@ __device__ __forceinline__ void project_fm_body(const FusedArgs& f, int b, int t
       if (act) {
         // this item's k-steps of half h: ks = 16 h + kq * NKS + j, j < NKS = 16 / S
         const int ks0 = 16 * h + kq * (16 / S);
+        const bool primed = h == 0;
         switch (S) {
-          case 1: fm_ksteps<16>(w3, n_rt, rt, ks0, h, lds, acc); break;
-          case 2: fm_ksteps<8>(w3, n_rt, rt, ks0, h, lds, acc); break;
-          case 4: fm_ksteps<4>(w3, n_rt, rt, ks0, h, lds, acc); break;
-          default: fm_ksteps<2>(w3, n_rt, rt, ks0, h, lds, acc); break;
+          case 1: fm_ksteps<16>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
+          case 2: fm_ksteps<8>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
+          case 4: fm_ksteps<4>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
+          default: fm_ksteps<2>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
         }
       }
     }
