@@ -29,5 +29,7 @@ has sweep && run sweep 300 python bench.py --sweep --steps 10 --warmup 2 --no-cp
 has rvqprof && run rvqprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_rvq -o run --output-format csv -- python tools/rvq_bench.py --batch 32 --nq 8 --iters 20 --paths fm
 has prof && run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 has profnp && run profnp 300 env VRVQ_CONV_PLANES=0 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_np -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+has long && run long_tests 500 $PT tests/test_gpu_long_clip.py
+has bench10 && run bench10 400 python bench.py --clip-seconds 10 --batch 1 --sweep --steps 5 --warmup 2 --no-cpu-baseline
 has all && run gpu_tests 1000 $PT tests -m gpu
 exit 0
