@@ -510,6 +510,33 @@ def test_full_train_step_runs(manifest):
     assert moved == len(before)
 
 
+def test_train_step_config4_shape():
+    """BASELINE configs[3]'s per-GPU shape (B = 32 x 0.38 s, vrvq_a2, the bench.py --train step):
+    two identically seeded states take one full step on the same batch -- every loss finite and
+    bitwise equal, every parameter bitwise equal afterwards (fixed-order reductions throughout,
+    discriminator convolutions included)."""
+    from vrvq_amd.config import A2_KWARGS
+    from vrvq_amd.recipe import synthetic_audio
+    from vrvq_amd.trainer import LAMBDAS_A2, build_state, train_step
+    x = torch.from_numpy(synthetic_audio(32, 16758, seed=4321)).to(DEV)
+    outs, params = [], []
+    for _ in range(2):
+        model = vrvq_amd.DAC_VRVQ(**A2_KWARGS)
+        load_recipe(model, 0)
+        torch.manual_seed(0)
+        state = build_state(model, DEV)
+        torch.manual_seed(1)
+        out = train_step(state, x, LAMBDAS_A2)
+        torch.cuda.synchronize()
+        outs.append({k: v.detach().clone() for k, v in out.items()})
+        params.append([p.detach().clone() for p in model.parameters()])
+        del state, model
+    for k, v in outs[0].items():
+        assert torch.isfinite(v).all(), k
+        assert torch.equal(v, outs[1][k]), k
+    assert all(torch.equal(a, b) for a, b in zip(*params))
+
+
 def _gen_ddp_worker(rank, world, port, q):
     import os
     import torch.distributed as dist

@@ -36,7 +36,7 @@ def main():
                     help="the frame-major launch (vrvq_rvq_encode_fm: chain parts project their "
                          "own frames)")
     args = ap.parse_args()
-    lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", "libvrvq_hip_stamps.so"))
+    lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", os.environ.get("VRVQ_STAMPS_LIB", "libvrvq_hip_stamps.so")))
     lib.vrvq_rvq_path.restype = ctypes.c_int
     assert lib.vrvq_rvq_path(2) in (1, 2)
     dev = torch.device("cuda:0")
@@ -135,7 +135,11 @@ def main():
     print("expansion workgroups")
     row("start", ex[:, 0])
     for i in range(nq):
+        if i < 8:
+            row(f"stage {i} slice seen (thread 0)", ex[:, 56 + i])
         row(f"stage {i} start", ex[:, 1 + i])
+        if i < 8:
+            row(f"stage {i} stores issued (thread 0)", ex[:, 48 + i])
     row("stages done", ex[:, 40])
     row("z_q stored", ex[:, 41])
     end = max(us(pc[:, 36]).max(), us(ex[:, 41]).max())

@@ -1338,6 +1338,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
         if (!late(g, i)) break;
       }
     }
+    if (i < 8) FSTAMP(f.stamps, 56 + i);  // the stage's slice seen (diagnostic build)
     float* slab = sm + (i & 1) * (FU_FB * RCD);
     *reinterpret_cast<float2*>(slab + fi * RCD + 2 * dp) =
         make_float2(__uint_as_float(g[0]), __uint_as_float(g[2]));
@@ -1385,6 +1386,7 @@ __device__ __forceinline__ void fused_expand_body(const FusedArgs& f, int e, flo
         zq[j][r] = zq[j][r] + q[r] * m;
       }
     }
+    if (i < 8) FSTAMP(f.stamps, 48 + i);  // the stage's stores issued (diagnostic build)
     cur = nxt;
   }
   FSTAMP(f.stamps, 40);
