@@ -1484,6 +1484,12 @@ __host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
 // NKS consecutive k-steps (32 channels each) of one 16-row tile against the staged K-half:
 // the A planes come from L2 in a ring three k-steps deep (36 VGPRs in flight per lane), each
 // k-step's six products in the x3 order m m, h l, l h, h m, m h, h h.
+#ifdef VRVQ_PJ_ROT
+// timing experiment only (another k order per workgroup: not bit-identical across positions)
+#define FM_ROT(j) (((j) + (int)blockIdx.x) % NKS)
+#else
+#define FM_ROT(j) (j)
+#endif
 constexpr int FM_DEPTH = 3, FM_PRIME = 1;  // ring depth; k-steps primed under the z loads
 template <int NKS>
 __device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
@@ -1495,7 +1501,7 @@ __device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt,
   for (int j = 0; j < DEPTH; ++j)
     if (j >= j0 && j < j1)
 #pragma unroll
-    for (int p = 0; p < 3; ++p) a[j][p] = w3[((size_t)((ks0 + j) * 3 + p) * n_rt + rt) * 64 + lane];
+    for (int p = 0; p < 3; ++p) a[j][p] = w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
 }
 // (primed: the ring's first DEPTH k-steps are already in flight in `a`, fm_prime)
 template <int NKS>
@@ -1506,12 +1512,12 @@ __device__ __forceinline__ void fm_ksteps(const u32x4* __restrict__ w3, int n_rt
   const int lane = threadIdx.x & 63, lr = lane & 15, kg = lane >> 4;
   auto load_a = [&](int j, u32x4 (&dst)[3]) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) dst[p] = w3[((size_t)((ks0 + j) * 3 + p) * n_rt + rt) * 64 + lane];
+    for (int p = 0; p < 3; ++p) dst[p] = w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
   };
   fm_prime<NKS>(w3, n_rt, rt, ks0, a, primed ? FM_PRIME : 0, FM_DEPTH);
 #pragma unroll
   for (int j = 0; j < NKS; ++j) {
-    const int kk = (ks0 + j - 16 * h) * 32 + 8 * kg;  // channel within the half
+    const int kk = (ks0 + FM_ROT(j) - 16 * h) * 32 + 8 * kg;  // channel within the half
     const char* bp = lds + lr * (LP_LD * 2) + kk * 2;
     const u32x4 bh = *reinterpret_cast<const u32x4*>(bp);
     const u32x4 bm = *reinterpret_cast<const u32x4*>(bp + LP_PLANE);
