@@ -513,8 +513,13 @@ def test_full_train_step_runs(manifest):
 def test_train_step_config4_shape():
     """BASELINE configs[3]'s per-GPU shape (B = 32 x 0.38 s, vrvq_a2, the bench.py --train step):
     two identically seeded states take one full step on the same batch -- every loss finite and
-    bitwise equal, every parameter bitwise equal afterwards (fixed-order reductions throughout,
-    discriminator convolutions included)."""
+    bitwise equal (the forward is deterministic), the gradient norms within 1e-5 and every
+    parameter within 2.5 lr of the other run's: the generator's gradient through the
+    discriminator comes from MIOpen's backward-data convolutions, which accumulate in a
+    run-dependent order (measured 3250.7571 vs 3250.7561 for the generator's gradient norm), and
+    AdamW's first step moves a parameter by ~lr * sign(grad), so a near-zero gradient element may
+    move either way; the HIP kernels' own gradients are bitwise deterministic
+    (test_train_step_deterministic)."""
     from vrvq_amd.config import A2_KWARGS
     from vrvq_amd.recipe import synthetic_audio
     from vrvq_amd.trainer import LAMBDAS_A2, build_state, train_step
@@ -533,8 +538,13 @@ def test_train_step_config4_shape():
         del state, model
     for k, v in outs[0].items():
         assert torch.isfinite(v).all(), k
-        assert torch.equal(v, outs[1][k]), k
-    assert all(torch.equal(a, b) for a, b in zip(*params))
+        if "grad_norm" in k:
+            assert rel_err(v.cpu().numpy(), outs[1][k].cpu().numpy()) < 1e-5, k
+        else:
+            assert torch.equal(v, outs[1][k]), k
+    lr = 1e-4  # trainer.build_state default (conf/base.yml)
+    for a, b in zip(*params):
+        assert float((a - b).abs().max()) <= 2.5 * lr
 
 
 def _gen_ddp_worker(rank, world, port, q):
