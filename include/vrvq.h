@@ -304,7 +304,9 @@ int vrvq_rvq_timing_read(float* mean_ms, int* count);
  * and expressions as vrvq_rvq_encode. w3in = vrvq_rvq_pack_w_in(w_in_t) (once per weight
  * version, vrvq_rvq_w_in_planes_size uint16 elements). Hand-off granules: eager calls use a
  * library-owned area per (device, stream) (workspace may be NULL); under stream capture pass a
- * workspace of >= vrvq_rvq_workspace_fm bytes (zeroed by captured memsets). VRVQ_ERR_UNSUPPORTED
+ * workspace of >= vrvq_rvq_workspace_fm bytes (zeroed by captured memsets; its first 8448 bytes
+ * are then the launch's sync block, word 2048 its wait status -- vrvq_rvq_sync_error covers
+ * eager calls only; the host-mapped word of vrvq_rvq_pending_error covers both). VRVQ_ERR_UNSUPPORTED
  * when the shape does not fit the launch (the caller then transposes and takes
  * vrvq_rvq_encode). Replaces models/quantize.py:353-365, 389-421 like vrvq_rvq_encode. */
 int vrvq_rvq_w_in_planes_size(int nq, int dim, int cdim, long long* n_u16);

@@ -1825,6 +1825,7 @@ struct FusedLaunch {
 
 // Sync block, epoch and granule area for one fused launch of `bytes` granules on st; false:
 // the fused launch cannot run now (the caller takes another path).
+constexpr size_t FU_SYNC_BYTES = (SYNC_WORDS * sizeof(unsigned) + 255) & ~size_t(255);
 bool fused_prepare(hipStream_t st, size_t bytes, void* caller_ws, size_t caller_bytes,
                    FusedLaunch* L) {
   int device = 0;
@@ -1842,24 +1843,27 @@ bool fused_prepare(hipStream_t st, size_t bytes, void* caller_ws, size_t caller_
       if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) g_err_host_dev = static_cast<unsigned*>(d);
     }
   }
-  StreamState& ss = g_fu[{device, st}];
   const size_t sync_bytes = SYNC_WORDS * sizeof(unsigned);
+  if (capturing) {
+    // no allocation inside a capture (and the capture stream is usually new to us): the sync
+    // block and the granule area both come from the caller's workspace, zeroed by memset nodes
+    // (the workspace functions count FU_SYNC_BYTES in)
+    if (!caller_ws || caller_bytes < bytes + FU_SYNC_BYTES) return false;
+    if (hipMemsetAsync(caller_ws, 0, bytes + FU_SYNC_BYTES, st) != hipSuccess) return false;
+    L->sync = static_cast<unsigned*>(caller_ws);
+    L->area = static_cast<char*>(caller_ws) + FU_SYNC_BYTES;
+    L->epoch = 1;
+    return true;
+  }
+  StreamState& ss = g_fu[{device, st}];
   if (!ss.sync) {
-    if (capturing) return false;  // no allocation inside a capture: another path this time
     if (hipMalloc(&ss.sync, sync_bytes) != hipSuccess) {
       ss.sync = nullptr;
       return false;
     }
     if (hipMemsetAsync(ss.sync, 0, sync_bytes, st) != hipSuccess) return false;
   }
-  if (capturing) {
-    if (!caller_ws || caller_bytes < bytes) return false;
-    if (hipMemsetAsync(ss.sync, 0, sync_bytes, st) != hipSuccess ||
-        hipMemsetAsync(caller_ws, 0, bytes, st) != hipSuccess)
-      return false;
-    L->area = static_cast<char*>(caller_ws);
-    L->epoch = 1;
-  } else {
+  {
     if (ss.area_bytes < bytes) {
       if (ss.area) {
         if (hipStreamSynchronize(st) != hipSuccess) return false;
@@ -2194,7 +2198,7 @@ extern "C" int vrvq_rvq_workspace(int batch, int frames, int nq, long long* byte
   const long long nf = (long long)batch * frames;
   // the fused path's partials are tagged granules (2 floats each)
   *bytes = (long long)(2 * part_floats(nf, nq) + zst_floats(batch, frames, nq)) *
-           (long long)sizeof(float);
+               (long long)sizeof(float) + (long long)FU_SYNC_BYTES;
   return 0;
 }
 
@@ -2345,7 +2349,7 @@ extern "C" int vrvq_rvq_workspace_fm(int batch, int frames, int nq, int ncode, l
   const int F = fm_frames_per_part(frames, nq, ncode);
   if (F < 1) return VRVQ_ERR_UNSUPPORTED;
   const int P = (frames + F - 1) / F;
-  *bytes = (long long)zsh_bytes(batch, nq, P);
+  *bytes = (long long)zsh_bytes(batch, nq, P) + (long long)FU_SYNC_BYTES;
   return 0;
 }
 
