@@ -1490,7 +1490,12 @@ __host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
 #else
 #define FM_ROT(j) (j)
 #endif
-constexpr int FM_DEPTH = 3, FM_PRIME = 1;  // ring depth; k-steps primed under the z loads
+#ifdef VRVQ_PJ_2PL
+#define FM_PL(p) ((p) == 2 ? -1 : (p))  // timing experiment only: two of the three W planes
+#else
+#define FM_PL(p) (p)
+#endif
+constexpr int FM_DEPTH = 4, FM_PRIME = 1;  // ring depth; k-steps primed under the z loads
 template <int NKS>
 __device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
                                          u32x4 (&a)[FM_DEPTH][3], int j0 = 0,
@@ -1501,7 +1506,7 @@ __device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt,
   for (int j = 0; j < DEPTH; ++j)
     if (j >= j0 && j < j1)
 #pragma unroll
-    for (int p = 0; p < 3; ++p) a[j][p] = w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
+    for (int p = 0; p < 3; ++p) a[j][p] = FM_PL(p) < 0 ? a[j][0] : w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
 }
 // (primed: the ring's first DEPTH k-steps are already in flight in `a`, fm_prime)
 template <int NKS>
@@ -1512,7 +1517,7 @@ __device__ __forceinline__ void fm_ksteps(const u32x4* __restrict__ w3, int n_rt
   const int lane = threadIdx.x & 63, lr = lane & 15, kg = lane >> 4;
   auto load_a = [&](int j, u32x4 (&dst)[3]) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) dst[p] = w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
+    for (int p = 0; p < 3; ++p) dst[p] = FM_PL(p) < 0 ? dst[0] : w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
   };
   fm_prime<NKS>(w3, n_rt, rt, ks0, a, primed ? FM_PRIME : 0, FM_DEPTH);
 #pragma unroll
