@@ -711,6 +711,8 @@ def _rvq_both_paths(nq, ncode, B, T, imp_on, zqis, seed, repeats=3, side_load=Fa
         got = []
         side = torch.cuda.Stream() if side_load else None
         a = torch.randn(2048, 2048, device=DEV) if side_load else None
+        _lib.rvq_timing_read()  # forget earlier timed launches
+        _lib.rvq_timing(True)   # counts the fused launches that actually ran
         for r in range(repeats):
             if side is not None:  # uneven load: a GEMM stream on part of the chip meanwhile
                 side.wait_stream(torch.cuda.current_stream())
@@ -719,9 +721,14 @@ def _rvq_both_paths(nq, ncode, B, T, imp_on, zqis, seed, repeats=3, side_load=Fa
                         a = (a @ a) * (1.0 / 2048)
             got.append(run())
         torch.cuda.synchronize()
+        _lib.rvq_timing(False)
+        _ms, launched = _lib.rvq_timing_read()
         assert _lib.rvq_sync_error(torch.cuda.current_stream().cuda_stream) == 0
     finally:
+        _lib.rvq_timing(False)
         _lib.rvq_path(prev)
+    # the fused launch ran (one per <= 32 clips) for T <= 96, none above (no silent fallback)
+    assert launched == (repeats * ((B + 31) // 32) if T <= 96 else 0), launched
     names = ("codes", "latents", "loss_pf", "z_q_is", "z_q", "mask")
     for g in got:
         for name, x, y in zip(names, want, g):

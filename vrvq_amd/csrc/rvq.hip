@@ -8,7 +8,10 @@
 // By linearity z_e(i) = ((P_i + b_in(i)) - Qb_i) - sum_{j<i} M_ij zst_j with P_i = W_in(i) z,
 // M_ij = W_in(i) W_out(j) (8x8) and Qb_i = W_in(i) sum_{j<i} b_out(j): the sequential part
 // lives in the 8-dim latent space and the 1024-dim work becomes two embarrassingly parallel
-// streams. Three launches:
+// streams. The product path is ONE launch (rvq_fm_kernel: chain parts project their own frames
+// of the encoder's frame-major z, expansion workgroups write z_q_is / z_q; rvq_fused_kernel:
+// the same on channel-major z for T <= 96, with projection units); both are built from the
+// bodies of the three-launch form, which stays as the reference path:
 //
 //   rvq_project_kernel   P partials over 8 channel splits (v_mfma_f32_16x16x4_f32): each
 //                        workgroup streams a 48-frame tile of one clip's 128-channel slab of
@@ -23,8 +26,11 @@
 //                        the matrix cores (32-channel x 32-frame tiles, bias as a 9th k): the
 //                        HBM write stream, with no LDS and a few VALU per element.
 //
-// Codes of every golden fixture are reproduced bit for bit (the same fp32 expression for the
-// distance as the reference: dot in k order, fma(d, -2, e2) + c2, lowest index on ties).
+// The distance is the reference's fp32 expression (dot in k order, fma(d, -2, e2) + c2, lowest
+// index on ties); the projection on the split-bf16 matrix cores (x3) is fp32-accurate but not
+// the reference's summation order, so the codes match every golden fixture BY TEST (full
+// batches included), not by construction: a near-tie could differ. The fp32-input projection
+// (vrvq_rvq_project_variant 2, rvq_project2_kernel) stays available as the exactness fallback.
 #include <hip/hip_ext.h>
 
 #include <map>
