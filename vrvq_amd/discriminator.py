@@ -9,6 +9,7 @@ the reference — `discriminators.<i>.convs.<j>.0.weight_g` etc. — so referenc
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Sequence, Tuple
 
 import torch
@@ -36,6 +37,32 @@ def _run(layers, x, fmap: list):
 _MPD_LAYERS = [(1, 32, 3), (32, 128, 3), (128, 512, 3), (512, 1024, 3), (1024, 1024, 1)]
 
 
+# The period discriminators' (k, 1) Conv2d run as Conv1d over the folded batch (B * period, C,
+# frames): the same sums per output element (each column is an independent 1-D signal); the
+# feature maps are then laid out (B * period, C, frames), which every use of them (means and
+# elementwise L1 between real and fake, losses.GANLoss) is invariant to. VRVQ_MPD_1D=0: the
+# reference's Conv2d over (B, C, frames, period).
+MPD_1D = os.environ.get("VRVQ_MPD_1D", "1") != "0"
+# ... and as plain GEMMs (hipBLASLt fp32) over a channels-last (B * period, frames, C) layout:
+# the k-tap windows of the strided conv gathered once (unfold), no layout transposes between
+# layers (VRVQ_MPD_GEMM=0: F.conv1d, MIOpen).
+MPD_GEMM = os.environ.get("VRVQ_MPD_GEMM", "1") != "0"
+
+
+def _conv1d_cl(h: torch.Tensor, w: torch.Tensor, bias, stride: int, pad: int) -> torch.Tensor:
+    """Conv1d on channels-last h (N, L, C) with w (Cout, C, k): (N, Lout, Cout), the k windows
+    of stride `stride` flattened (tap, channel) against w laid out (Cout, k, C)."""
+    n, _, c = h.shape
+    cout, _, k = w.shape
+    hp = F.pad(h, (0, 0, pad, pad))
+    win = hp.unfold(1, k, stride)                      # (N, Lout, C, k) view
+    lout = win.shape[1]
+    cols = win.transpose(2, 3).reshape(n * lout, k * c)  # (tap, channel) per row: one copy
+    wm = w.permute(0, 2, 1).reshape(cout, k * c)
+    y = torch.addmm(bias, cols, wm.t()) if bias is not None else cols @ wm.t()
+    return y.reshape(n, lout, cout)
+
+
 class MPD(nn.Module):
     """Period discriminator: the waveform folded into `period` columns (:30-65)."""
 
@@ -52,6 +79,22 @@ class MPD(nn.Module):
         b, c, n = x.shape
         x = x.reshape(b, c, n // self.period, self.period)
         fmap: list = []
+        if MPD_1D:
+            # (B, C, frames, period) -> (B * period, C, frames) or channels-last (.., frames, C)
+            h = x.permute(0, 3, 1, 2).reshape(b * self.period, c, n // self.period)
+            if MPD_GEMM:
+                h = h.transpose(1, 2)
+            for layer in list(self.convs) + [self.conv_post]:
+                conv = layer[0] if isinstance(layer, nn.Sequential) else layer
+                w = torch._weight_norm(conv.weight_v, conv.weight_g, 0)[..., 0]
+                if MPD_GEMM:
+                    h = _conv1d_cl(h, w, conv.bias, conv.stride[0], conv.padding[0])
+                else:
+                    h = F.conv1d(h, w, conv.bias, stride=conv.stride[0], padding=conv.padding[0])
+                if layer is not self.conv_post:
+                    h = F.leaky_relu(h, 0.1)
+                fmap.append(h)
+            return fmap
         x = _run(self.convs, x, fmap)
         fmap.append(self.conv_post(x))
         return fmap
