@@ -1175,7 +1175,35 @@ struct FusedArgs {
   unsigned epoch;
   unsigned long long* stamps;       // diagnostic build only
   int dbg;                          // diagnostic build only: bit 0 = expansion skips its MFMAs
+  int warm;                         // expansion workgroups pull the stage tables into L2 first
 };
+
+// The stage tables the chain and the expansion read after stage 0 (normalised / raw codebooks,
+// c2, M, W_out, b_out): inside the bench step the encoder's convs have evicted them from L2, and
+// the expansion workgroups idle until the chain's first stage anyway. Expansion workgroup e of
+// the launch touches slice (e / 8) of every table (workgroups are dealt to the 8 XCDs in turn,
+// so each XCD's L2 gets a whole copy); the loaded values feed a sum nothing uses.
+__device__ __forceinline__ void warm_tables(const FusedArgs& f, int e, int n_exp, int N,
+                                            float* sm) {
+  const int slices = max(1, n_exp / 8), k = (e / 8) % slices;
+  const size_t nq = (size_t)f.c.nq;
+  unsigned acc = 0;
+  auto touch = [&](const float* p, size_t n) {  // n floats, a multiple of 4
+    const size_t per = ((n / 4 + slices - 1) / slices) * 4;
+    const size_t lo = (size_t)k * per, hi = min(n, lo + per);
+    for (size_t i = lo + 4 * threadIdx.x; i < hi; i += 4 * blockDim.x) {
+      const float4 v = ld4(p + i);
+      acc ^= __float_as_uint(v.x) ^ __float_as_uint(v.w);
+    }
+  };
+  touch(f.c.cbf, nq * N * RCD);
+  touch(f.c.cb, nq * N * RCD);
+  touch(f.c.c2, nq * N);
+  touch(f.c.mcol, nq * nq * RCD * RCD);
+  touch(f.w_out, nq * RD * RCD);
+  touch(f.b_out, nq * RD);
+  if (acc == f.spin_max + 0x5a5a5a5au) sm[threadIdx.x] = __uint_as_float(acc);  // never in practice
+}
 
 // Expansion workgroup (clip b, frames [128 fb, +128), channels [128 cb, +128)): wave w =
 // 32-channel tile (w & 3) x 32-frame tiles {w >> 2, (w >> 2) + 2} of the block; per stage four
@@ -1659,6 +1687,7 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fm_kernel(FusedArgs f) {
   const int blk = blockIdx.x;
   FSTAMP(f.stamps, 0);
   if (blk >= B * f.P) {
+    if (f.warm) warm_tables(f, blk - B * f.P, (int)gridDim.x - B * f.P, 256 * NM, sm);
     fused_expand_body(f, blk - B * f.P, sm);
     FSTAMP(f.stamps, 41);
     return;
@@ -2384,6 +2413,12 @@ extern "C" int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frame
   f.w3in = reinterpret_cast<const u32x4*>(w3in);
   f.w_out = w_out;
   f.b_out = b_out;
+  // VRVQ_RVQ_WARM=0: the expansion workgroups do not pull the stage tables into L2 (A/B)
+  static const int warm = [] {
+    const char* e = getenv("VRVQ_RVQ_WARM");
+    return e ? atoi(e) : 1;
+  }();
+  f.warm = warm;
   hipStream_t st = as_stream(stream);
   const size_t wsb = (size_t)workspace_bytes;
   switch (ncode / 256) {
