@@ -64,8 +64,11 @@ def test_argument_errors_raise_before_launch():
     assert lib.vrvq_rvq_workspace(32, 87, 8, ctypes.byref(n)) == 0
     # partials as tagged granules (8 B each, the fused launch) + the larger of the zst rows
     # (B T nq d floats) and the fused launch's tagged stage granules (B nq 8 parts x 16 frames
-    # x d x 8 B)
-    assert n.value == (2 * 8 * 32 * 87 * 64 + max(32 * 87 * 8 * 8, 32 * 8 * 8 * 16 * 8 * 2)) * 4
+    # x d x 8 B), then the sync block a captured fused launch takes from the workspace (2052
+    # words, rounded up to 256 B)
+    sync = (2052 * 4 + 255) // 256 * 256
+    assert n.value == (2 * 8 * 32 * 87 * 64 + max(32 * 87 * 8 * 8, 32 * 8 * 8 * 16 * 8 * 2)) * 4 \
+        + sync
     assert lib.vrvq_rvq_path(7) == 10001 and lib.vrvq_rvq_path(0) in (1, 2)
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)

@@ -28,9 +28,31 @@ def test_discriminator_forward_shapes():
     fm = d(torch.randn(2, 1, 4410) * 0.1)
     assert len(fm) == 8
     assert [len(f) for f in fm] == [6] * 5 + [26] * 3
-    for f in fm:
+    for p, f in zip([2, 3, 5, 7, 11], fm[:5]):
+        # period discriminators: channels-last over the folded batch (B * period, frames, 1)
+        assert f[-1].shape[0] == 2 * p and f[-1].shape[2] == 1
+    for f in fm[5:]:
         assert f[-1].shape[0] == 2 and f[-1].shape[1] == 1
+    for f in fm:
         assert all(torch.isfinite(t).all() for t in f)
+
+
+def test_mpd_folded_gemm_matches_conv2d(monkeypatch):
+    """The folded channels-last GEMM form of a period discriminator holds the reference's
+    Conv2d feature maps (models/discriminator.py:30-65), element for element."""
+    import vrvq_amd.discriminator as D
+
+    torch.manual_seed(1)
+    mpd = D.MPD(3)
+    x = torch.randn(2, 1, 997) * 0.1
+    fm = mpd(x)
+    monkeypatch.setattr(D, "MPD_1D", False)
+    ref = mpd(x)
+    assert len(fm) == len(ref) == 6
+    for a, r in zip(fm, ref):
+        b, c, frames, p = r.shape
+        got = a.reshape(b, p, frames, c).permute(0, 3, 2, 1)
+        torch.testing.assert_close(got, r, rtol=1e-4, atol=1e-6)
 
 
 def test_stft_match_stride_frames():
