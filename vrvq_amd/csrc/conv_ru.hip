@@ -32,13 +32,20 @@ struct RuArgs {
   const float* w1;     // [C][1][m_pad]  packed k=1 weight
   const u32x4* w1x3;   // pre-split W1 (vrvq_pack_x3_weight, k = 1) or null
   int C;
+  int p2h;             // ru_p2x3h tiles: phase 2 on the split MFMA in two K-halves (else fp32)
 };
 
 // Phase 2 on the split bf16 MFMA when its three hs planes (6 B per element) fit in the LDS
 // the kernel already holds: C = 64 / 96 / 192 (C = 128 at BN = 128 would need 96 KiB and
-// drop to one workgroup per CU; it keeps the fp32 phase 2).
+// drop to one workgroup per CU: it runs phase 2 in two K-halves, ru_p2x3h).
 template <int BM, int BN>
 constexpr bool ru_p2x3() { return BM * BN * 6 <= 80 * 1024; }
+// ... else in two K-halves (half the planes + the other half parked as fp32) where that fits:
+// C = 128 at BN = 128 (rows split over two wave rows)
+template <int BM, int BN, int WM>
+constexpr bool ru_p2x3h() {
+  return !ru_p2x3<BM, BN>() && WM == 2 && BM % 32 == 0 && BM * BN * 5 <= 80 * 1024;
+}
 
 template <int BM, int BN, int WM, int NW, bool X3>
 __global__ __launch_bounds__(64 * NW)
@@ -172,6 +179,127 @@ void ru_fused_kernel(RuArgs ra) {
     }
   }
 
+  if constexpr (X3 && ru_p2x3h<BM, BN, WM>()) {
+    if (ra.w1x3 != nullptr && ra.p2h) {
+      // ---- phase 2 on the split bf16 MFMA in two K-halves (C = 128 at BN = 128: the three
+      // planes of all 128 channels would take 96 KB). The wm = 0 waves hold rows [0, 64): they
+      // write them as half 0's planes [plane][8 octets][BN][8] (48 KB); the wm = 1 waves park
+      // rows [64, 128) as fp32 snake2(h + b7) [64][BN] behind them (32 KB): 80 KB, still two
+      // workgroups per CU. Half 0's eight K-steps run, the parked rows are split into the same
+      // planes, half 1's run: the octet order of the x3 k = 1 conv, so the unit is bit-identical
+      // to the two launches, as for C = 64 / 96 / 192.
+      constexpr int HC8 = BM / 16;  // channel octets per half
+      constexpr int HQ = BM / 32;   // K-steps (16 channels) per half
+      char* hsb = reinterpret_cast<char*>(smem);
+      float* park = reinterpret_cast<float*>(hsb + (size_t)3 * HC8 * BN * 16);
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row0 = wm * TM + i * 32 + 8 * g + 4 * lh;
+          float bb[4], al[4], ia[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = row0 + u < C;
+            bb[u] = ok ? ra.b7[row0 + u] : 0.0f;
+            al[u] = ok ? ra.alpha2[row0 + u] : 0.0f;
+            ia[u] = ok ? ra.inv_alpha2[row0 + u] : 0.0f;
+          }
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = acc[i][j][4 * g + u] + bb[u];
+            snake_n<4>(v, al, ia);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = row0 + u < C ? v[u] : 0.0f;
+            const int col = wn * TN + j * 32 + lr;
+            if (row0 < BM / 2) {  // wave-uniform (wm)
+              unsigned h[2], m[2], l[2];
+              split3x2(v[0], v[1], h[0], m[0], l[0]);
+              split3x2(v[2], v[3], h[1], m[1], l[1]);
+              const size_t off = ((size_t)(row0 >> 3) * BN + col) * 16 + lh * 8;
+              *reinterpret_cast<u32x2*>(hsb + off) = u32x2{h[0], h[1]};
+              *reinterpret_cast<u32x2*>(hsb + (size_t)HC8 * BN * 16 + off) = u32x2{m[0], m[1]};
+              *reinterpret_cast<u32x2*>(hsb + 2 * (size_t)HC8 * BN * 16 + off) = u32x2{l[0], l[1]};
+            } else {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) park[(row0 - BM / 2 + u) * BN + col] = v[u];
+            }
+          }
+        }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+      const u32x4* hs = reinterpret_cast<const u32x4*>(hsb);
+      auto lda = [&](int q, u32x4 (&av)[3][RM]) {
+        const int o = 2 * q + lh;  // global octet; k = 1 packing: chunks of 4 octets
+        const int ch = o >> 2, oo = o & 3;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+            av[p][i] = ra.w1x3[((size_t)(ch * 3 + p) * 4 + oo) * a.m_pad + wm * TM + i * 32 + lr];
+      };
+      u32x4 an[3][RM];
+      lda(0, an);
+      auto steps = [&](int q0) {  // K-steps q0 .. q0 + HQ - 1 against the half in the planes
+#pragma unroll 2
+        for (int q = q0; q < q0 + HQ; ++q) {
+          u32x4 ac[3][RM], bv[3][RN];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int i = 0; i < RM; ++i) ac[p][i] = an[p][i];
+          lda(min(q + 1, 2 * HQ - 1), an);
+          const int o = 2 * (q - q0) + lh;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              bv[p][j] = hs[((size_t)p * HC8 + o) * BN + wn * TN + j * 32 + lr];
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j) {
+              f32x16 t = acc[i][j];
+              t = mfma_bf16(ac[1][i], bv[1][j], t);  // m m
+              t = mfma_bf16(ac[0][i], bv[2][j], t);  // h l
+              t = mfma_bf16(ac[2][i], bv[0][j], t);  // l h
+              t = mfma_bf16(ac[0][i], bv[1][j], t);  // h m
+              t = mfma_bf16(ac[1][i], bv[0][j], t);  // m h
+              acc[i][j] = mfma_bf16(ac[0][i], bv[0][j], t);  // h h
+            }
+        }
+      };
+      steps(0);
+      __syncthreads();  // half 0's planes no longer read
+      for (int e = tid; e < HC8 * BN; e += 64 * NW) {  // the parked rows -> half 1's planes
+        const int c8 = e / BN, col = e - c8 * BN;
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = park[(c8 * 8 + u) * BN + col];
+        unsigned h[4], m[4], l[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) split3x2(v[2 * u], v[2 * u + 1], h[u], m[u], l[u]);
+        u32x4* dst = reinterpret_cast<u32x4*>(hsb) + (size_t)c8 * BN + col;
+        dst[0] = u32x4{h[0], h[1], h[2], h[3]};
+        dst[(size_t)HC8 * BN] = u32x4{m[0], m[1], m[2], m[3]};
+        dst[2 * (size_t)HC8 * BN] = u32x4{l[0], l[1], l[2], l[3]};
+      }
+      __syncthreads();
+      steps(HQ);
+      __syncthreads();  // hs reads done: the epilogue reuses the LDS
+      conv_epilogue<BM, BN, WM, NW>(ra.p2, smem, acc, b, 0, n0);
+      return;
+    }
+  }
+
   // ---- mid: hs[row][col] = snake2(h + b7) in the MFMA D layout (rows >= C: zero) ----
   float* hs = smem;
 #pragma unroll
@@ -254,8 +382,18 @@ static bool ru_bn64() {
   return v;
 }
 
+// tuning override: VRVQ_RU_P2H=0 keeps the C = 128 unit's phase 2 on the fp32 MFMA (A/B)
+static bool ru_p2_halves() {
+  static const bool v = [] {
+    const char* e = getenv("VRVQ_RU_P2H");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 template <int BM, int BN, int WM, int NW>
 int launch_ru(RuArgs ra, int batch, hipStream_t st) {
+  ra.p2h = ru_p2_halves() ? 1 : 0;
   constexpr int CK = ChunkCfg<7, BM, BN>::CK;
   ConvArgs& a = ra.p1;
   a.n_mt = 1;
@@ -277,6 +415,9 @@ int launch_ru(RuArgs ra, int batch, hipStream_t st) {
     size_t lx = x3_lds_bytes<7, BM, BN>(XW, a.cin);
     if (lx < hsz) lx = hsz;
     if (ru_p2x3<BM, BN>() && ra.w1x3 != nullptr && lx < (size_t)BM * BN * 6) lx = (size_t)BM * BN * 6;
+    if (ru_p2x3h<BM, BN, WM>() && ra.w1x3 != nullptr && ru_p2_halves() &&
+        lx < (size_t)BM * BN * 5)
+      lx = (size_t)BM * BN * 5;
     if (lx < epi) lx = epi;
     if (a.w3 != nullptr && XW <= (BN - 1) + 6 * 9 + 1 && lx <= 160 * 1024 && ru_x3_ok(BM)) {
       if (lx > 64 * 1024) {
