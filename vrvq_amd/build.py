@@ -102,8 +102,19 @@ def build_torch_ops(verbose: bool = True) -> str:
     return TORCH_LIB
 
 
+def _objects_current() -> bool:
+    """Every object newer than its source and the headers (a source edited while a build ran
+    leaves the library newer than it but its object stale)."""
+    headers = [d for d in deps() if not d.endswith(".hip")]
+    for src in sources():
+        obj = os.path.join(OBJ_DIR, os.path.basename(src)[:-4] + ".o")
+        if not _newer(obj, headers + [src]):
+            return False
+    return True
+
+
 def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and _newer(LIB, deps()):
+    if not force and _newer(LIB, deps()) and (not os.path.isdir(OBJ_DIR) or _objects_current()):
         pass
     else:
         _compile_and_link(LIB, [], verbose, "")
