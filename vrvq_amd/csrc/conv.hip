@@ -544,6 +544,19 @@ static long long conv_bn96_min() {
   return v;
 }
 
+// The phase-split strided convs at T <= 96 (512 -> 1024 s8 at T = 87): tile width, fixed per
+// layer type (batch-invariant sums). Tuning override VRVQ_CONV_PH_T87=32 (default) | 96.
+// Measured (profiles/r05zf_t87_tiles_ab.txt): 96-wide 691 -> 629 us for that layer, bench
+// within the spread; the k3 layers at 96 (VRVQ_CONV_BN96_MIN=0) no faster. The layer is bound
+// by its 128-chunk serial K loop per workgroup, not by the weight re-streaming alone.
+static int conv_ph_t87() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_PH_T87");
+    return e && atoi(e) == 96 ? 96 : 32;
+  }();
+  return v;
+}
+
 // x3 k7 layers over long rows (M a multiple of 64 and >= 128, Cin a multiple of 16): 64 x 256
 // tiles on 16-channel "pair" K-chunks (conv_x3.h: no zero octet, 168 MFMAs per wave between
 // barriers). 384 x 384 k7 at T = 5568, B = 32: 2027 -> 755-796 us (0.43 -> 0.50 of the x3
@@ -596,7 +609,7 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     // instead (batch-invariant outputs, tests/test_gpu_parity.py test_batch_invariance_*): the
     // polyphase ConvTranspose (up > 0) 96-wide, the phase-split strided convs 32-wide -- what
     // configs[1] (B = 32) ran before.
-    if (KS == 2 && a.w3 != nullptr) bn = a.up > 0 ? 96 : 32;
+    if (KS == 2 && a.w3 != nullptr) bn = a.up > 0 ? 96 : conv_ph_t87();
   }
   // k = 16 (the stride-8 encoder convs): the 8 MB weight block does not fit in L2, so the
   // 128-wide tile's halved weight re-streaming beats its padding (1490 -> 1323 us at T = 696,
