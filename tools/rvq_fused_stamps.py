@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--fm", action="store_true",
                     help="the frame-major launch (vrvq_rvq_encode_fm: chain parts project their "
                          "own frames)")
+    ap.add_argument("--flags", type=int, default=0,
+                    help="timing experiment: vrvq_debug_set_fused_flags bits (2: the chain parts "
+                         "skip the next stage's codebook fragment loads; outputs not checked)")
     args = ap.parse_args()
+    flags = (1 if args.no_expand_mfma else 0) | args.flags
     lib = ctypes.CDLL(os.path.join(HERE, "vrvq_amd", os.environ.get("VRVQ_STAMPS_LIB", "libvrvq_hip_stamps.so")))
     lib.vrvq_rvq_path.restype = ctypes.c_int
     assert lib.vrvq_rvq_path(2) in (1, 2)
@@ -90,23 +94,24 @@ def main():
         run(False)
     run(True)
     torch.cuda.synchronize()
-    if args.no_expand_mfma:
-        lib.vrvq_debug_set_fused_flags(1)
+    if flags:
+        lib.vrvq_debug_set_fused_flags(flags)
         stamps.zero_()
         for _ in range(5):
             run(False)
         run(True)
         torch.cuda.synchronize()
         lib.vrvq_debug_set_fused_flags(0)
-        print("expansion MFMAs skipped (timing experiment)")
+        print(f"fused flags {flags} (timing experiment: 1 expansion MFMAs skipped, 2 chain "
+              "codebook stream skipped)")
     if args.fm:
         ref = vrvq_amd.ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
                                          st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
     else:
         ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
     nocheck = os.environ.get("VRVQ_STAMPS_NOCHECK") == "1"  # timing-only experiment builds
-    assert nocheck or torch.equal(ref[0], codes), "stamped build disagrees with the product library"
-    if args.no_expand_mfma:
+    assert nocheck or flags or torch.equal(ref[0], codes), "stamped build disagrees with the product library"
+    if flags:
         zq.copy_(ref[4])
     assert nocheck or torch.equal(ref[4], zq), "stamped build disagrees with the product library"
     if args.no_zqis:

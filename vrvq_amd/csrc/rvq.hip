@@ -658,6 +658,7 @@ struct ChainHandoff {              // fused launches only
   unsigned long long* zsh;         // this part's stage-0 block of tagged zst granules
   int zsh_stage;                   // granules per stage
   unsigned long long* stamps;      // diagnostic build only
+  int dbg;                         // diagnostic build only: FusedArgs::dbg
 };
 
 // Where a chain part gets pu = (P + b_in) - Qb of its frames: CH_SPLIT the 8 split partials of
@@ -917,6 +918,15 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
          // waitcnt pass assume none are outstanding at the join, so the candidate-row wait
          // below would drain the whole prefetch.
         const int in = more ? i + 1 : i;
+#ifdef VRVQ_STAMPS
+        if (FUSED && (hx.dbg & 2)) {  // timing experiment: no per-stage codebook stream
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            an[t][0] = av[t][0];
+            an[t][1] = av[t][1];
+          }
+        } else
+#endif
         load_a(in, an);
 #pragma unroll
         for (int q = 0; q < C2W; ++q)
@@ -1174,7 +1184,9 @@ struct FusedArgs {
   unsigned stall;                   // test knob: chain part 0's start delayed by stall x s_sleep(127)
   unsigned epoch;
   unsigned long long* stamps;       // diagnostic build only
-  int dbg;                          // diagnostic build only: bit 0 = expansion skips its MFMAs
+  int dbg;                          // diagnostic build only: bit 0 = expansion skips its MFMAs,
+                                    // bit 1 = chain parts skip the next stage's codebook
+                                    // fragment loads (outputs wrong; timing only)
   int warm;                         // expansion workgroups pull the stage tables into L2 first
 };
 
@@ -1446,6 +1458,7 @@ __device__ __forceinline__ ChainHandoff fused_handoff(const FusedArgs& f, int b,
   hx.zsh = f.zsh + (size_t)(b * f.c.nq * f.P + p) * FU_ROWS * RCD;
   hx.zsh_stage = f.P * FU_ROWS * RCD;
   hx.stamps = f.stamps;
+  hx.dbg = f.dbg;
   return hx;
 }
 
