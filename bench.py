@@ -50,16 +50,21 @@ SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
 # the reference inference driver's own sweep (scripts/inference.py:58-70: 10-s clips, 12 levels)
 LEVELS_INFERENCE = (0.2, 0.3, 0.4, 0.5, 0.6, 0.8, 1.0, 1.2, 1.5, 2.0, 2.5, 3.0)
-RVQ_KERNELS = ("rvq_fm_kernel", "rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
+RVQ_KERNELS = ("rvq_pt_kernel", "rvq_fm_kernel", "rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
                "rvq_chain_kernel", "rvq_expand_kernel")
 
 
-def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024) -> int:
-    """Algorithmic HBM bytes of one RVQ pass:
-    per frame z read, imp read, z_q_is + z_q writes, codes (int64), latents, mask, loss;
-    plus the stage weights (normalised codebook counted once more)."""
-    per_frame = D * 4 + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
-    weights = nq * 4 * (d * D + d + 2 * N * d + D * d + D)
+def rvq_bytes(B: int, T: int, nq: int, D: int = 1024, d: int = 8, N: int = 1024,
+              from_partials: bool = True) -> int:
+    """Algorithmic HBM bytes of one RVQ pass. SURVEY.md §8(d)'s count per frame: z read, imp
+    read, z_q_is + z_q writes, codes (int64), latents, mask, loss; plus the stage weights
+    (normalised codebook counted once more). from_partials (the eval encode's path: the encoder's
+    last conv computed every stage's in_proj in its epilogue, vrvq_conv1d_proj): the kernel reads
+    the 8 channel-split partials (8 x nq d fp32 per frame) instead of z (D fp32), and W_in is the
+    conv's read, not the quantizer's."""
+    inp = 8 * nq * d * 4 if from_partials else D * 4
+    per_frame = inp + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
+    weights = nq * 4 * ((0 if from_partials else d * D) + d + 2 * N * d + D * d + D)
     return B * T * per_frame + weights
 
 
@@ -185,7 +190,9 @@ class RvqTimer:
                 self.events.append((e0, e1))
                 return r
             return timed
-        # the channel-major entry and the frame-major one the eval encode takes (model.py RVQ_FM)
+        # the eval encode's entry (from the conv's partials, model.py RVQ_PROJ) and the
+        # frame-major / channel-major ones of the A/B paths
+        ops.rvq_encode_part = wrap(ops.rvq_encode_part)
         ops.rvq_encode = wrap(ops.rvq_encode)
         ops.rvq_encode_fm = wrap(ops.rvq_encode_fm)
 
@@ -441,12 +448,14 @@ def main(argv=None):
 
     res_t = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize, device=dev,
                         on_start=on, on_stop=off)
+    vrvq_amd.check_errors(dev)  # end of work: a timed-out RVQ hand-off raises here, not silently
     ms_per_step = res_t.seconds / args.steps * 1e3
     value = throughput(args.batch * clip / SR, res_t)
     T = math.ceil(clip / model.hop_length)
     rvq_ms = timer.mean_ms()
     kern_ms, kern_n, per_call = timer.kernel_ms()
-    byt = rvq_bytes(args.batch, T, nq)
+    from_part = vrvq_amd.model.RVQ_PROJ
+    byt = rvq_bytes(args.batch, T, nq, from_partials=from_part)
     # the dominant kernel's time per rvq_encode call (the fused launches of the call: one per 32
     # clips); the operator bracket when the shape takes the three launches (no kernel-attached
     # events there)
@@ -502,29 +511,38 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "RVQ path: one torch.ops.vrvq.rvq_encode_fm = rvq_fm_kernel, "
-                                   "one launch per <= 32 clips (chain parts project their own "
-                                   "frames of the encoder's frame-major z, then the stage chain; "
-                                   "expansion workgroups write z_q_is / z_q; in-launch tagged-"
-                                   "granule hand-offs)",
+                         "kernel": ("RVQ path: one torch.ops.vrvq.rvq_encode_part = "
+                                    "rvq_pt_kernel per group of resident clips (chain parts sum "
+                                    "the 8 channel-split in_proj partials the encoder's last conv "
+                                    "wrote in its epilogue, vrvq_conv1d_proj, then the stage "
+                                    "chain; expansion workgroups with a loader wave write z_q_is "
+                                    "/ z_q; in-launch tagged-granule hand-offs)"
+                                    if from_part else
+                                    "RVQ path: one torch.ops.vrvq.rvq_encode_fm = rvq_fm_kernel "
+                                    "per <= 32 clips (A/B path, VRVQ_RVQ_PROJ=0)"),
                          "bytes_per_call": byt,
+                         "bytes_model": ("SURVEY.md §8(d) with the kernel's input = the 8 "
+                                         "channel-split in_proj partials (8 x 8 nq fp32 per "
+                                         "frame) instead of z, W_in not read"
+                                         if from_part else "SURVEY.md §8(d)"),
+                         "bytes_per_call_survey_z_input": rvq_bytes(args.batch, T, nq,
+                                                                    from_partials=False),
                          "kernel_us": round(kern_ms * 1e3, 2) if kern_n else None,
                          "kernel_launches_timed": kern_n,
                          "launches_per_call": round(per_call, 3),
                          "path_us": round(rvq_ms * 1e3, 2),
                          "kernel_us_rocprof": split, "kernel_us_source": split_src},
             "roofline_conv": {"bound": "mfma", "achieved": round(conv_tflops, 2),
-                              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": round(conv_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                              "peak": round(X3_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+                              "frac": round(conv_tflops / X3_PEAK_TFLOPS, 4),
                               "flops_per_step": flops,
-                              "x3_peak": X3_PEAK_TFLOPS,
-                              "frac_x3": round(conv_tflops / X3_PEAK_TFLOPS, 4),
-                              "note": "algorithmic fp32 conv FLOPs / (step time - RVQ launches). "
-                                      "Stride-1 convs run the x3 path (csrc/conv_x3.h): both "
-                                      "operands split exactly into 3 bf16 terms, 6 bf16 MFMAs "
-                                      "per fp32 product pair, fp32 accumulate (fp32-accurate; "
-                                      "its ceiling x3_peak = bf16 dense peak / 6); peak = the "
-                                      "fp32-input MFMA peak the strided convs run on"},
+                              "note": "algorithmic fp32 conv FLOPs / (step time - RVQ launches) "
+                                      "against the x3 ceiling: every MFMA conv runs the x3 path "
+                                      "(csrc/conv_x3.h: both operands split exactly into 3 bf16 "
+                                      "terms, 6 bf16 MFMAs per fp32 product pair, fp32 "
+                                      "accumulate -- fp32-accurate), whose ceiling is the bf16 "
+                                      "dense peak / 6 = 419.4 TF/s; the fp32-input MFMA peak "
+                                      "(157.3 TF/s) is not this path's bound"},
         }
         if levels_rep is not None:
             res["levels"] = levels_rep

@@ -107,30 +107,6 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
-/* vrvq_conv1d with the bf16 "planes" layouts of a Snake-activated operand (csrc/conv_pl.h):
- *   y_snake_planes  (instead of y_snake) snake_out(y) as three bf16 planes [B][3][cout/8][tout][8]
- *                   (v = h + m + l exactly: the split the x3 staging would make; cout % 8 == 0,
- *                   16-byte aligned);
- *   x_planes != 0   x is such a planes tensor [B][3][cin/8][tin][8] holding snake(x) (alpha must
- *                   be NULL): the k7 "planes" tile (stride 1, pad 3 dil, w_x3 required,
- *                   cin % 16 == 0, cout % 64 == 0 and >= 128), whose K-chunk stages are filled by
- *                   LDS-DMA with no register staging; outputs bit-identical to the fp32-input
- *                   x3 k7 pair tile on the same values.
- * Used by the residual units' k7 -> k1 chain (models/layers.py:52-68). VRVQ_ERR_UNSUPPORTED
- * for shapes outside those. */
-int vrvq_conv1d_ex(const void* x, int x_planes, int batch, int cin, int tin, const float* alpha,
-                   const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
-                   int cout_pad, int k, int stride, int pad, int dil, const float* bias,
-                   const float* residual, int epilogue, float* y, int tout,
-                   const float* alpha_out, const float* inv_alpha_out, float* y_snake,
-                   uint16_t* y_snake_planes, vrvq_stream_t stream);
-/* vrvq_conv_transpose1d_pad with snake_out(y) as planes (strides 2 / 4 / 8, cout % 8 == 0). */
-int vrvq_conv_transpose1d_ex(const float* x, int batch, int cin, int tin, const float* alpha,
-                             const float* inv_alpha, const float* w_packed, const uint16_t* w_x3,
-                             int cout, int cout_pad, int stride, int pad, const float* bias,
-                             float* y, const float* alpha_out, const float* inv_alpha_out,
-                             float* y_snake, uint16_t* y_snake_planes, vrvq_stream_t stream);
-
 /* vrvq_conv1d (stride 1, no residual / epilogue / output Snake) writing y FRAME-MAJOR:
  * y_fm[b][t][co] (tout x cout per clip, cout % 4 == 0, 16-byte aligned) -- the encoder's last
  * conv (models/dac_vrvq.py:34) producing z in the layout of vrvq_rvq_encode_fm's zt, straight
@@ -153,6 +129,19 @@ int vrvq_conv1d_fm(const float* x, int batch, int cin, int tin, const float* alp
 int vrvq_x3_weight_size(int cin, int k, int cout_pad, long long* n_u16);
 int vrvq_pack_x3_weight(const float* w_packed, int cin, int k, int cout_pad, uint16_t* w_x3,
                         vrvq_stream_t stream);
+
+/* The encoder's last conv (Snake1d -> WNConv1d k3, models/dac_vrvq.py:33-34; stride 1, no
+ * residual / epilogue, cout == 1024) with the in_proj of every RVQ stage in its epilogue
+ * (models/quantize.py:65, VectorQuantize.in_proj applied to z for all stages at once, without
+ * bias): part[s][b*tout + t][r] = sum_{c in 128 s .. 128 s + 127} W_in[r][c] z[b][c][t] for the
+ * 8 channel splits s and r < 8 nq -- vrvq_rvq_project's partials bit for bit (its x3 variant),
+ * computed from the conv's accumulators, so the quantizer never reads z back (vrvq_rvq_encode_part
+ * takes part). w3in = vrvq_rvq_pack_w_in(w_in_t). y (nullable) also receives z [B][1024][tout]
+ * as vrvq_conv1d writes it. part: [8][B*tout][8 nq] fp32, 16-byte aligned. */
+int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, const float* alpha,
+                     const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
+                     int cout_pad, int k, int pad, int dil, const float* bias, float* y, int tout,
+                     const uint16_t* w3in, int nq, float* part, vrvq_stream_t stream);
 
 /* Pack a folded Conv1d weight w[Cout][Cin][k] into [Cin][k][cout_pad]. */
 int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,
@@ -320,6 +309,33 @@ int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frames, int nq, 
                        int64_t* codes, float* latents, float* loss_pf, float* z_q_is, float* z_q,
                        float* mask, void* workspace, long long workspace_bytes,
                        vrvq_stream_t stream);
+
+/* The whole quantizer from the projection partials of vrvq_conv1d_proj (the eval encode's path):
+ * ONE launch per group of resident clips (rvq_pt_kernel): chain parts (<= 16 frames of a clip)
+ * sum their frames' 8 partials in split order, run the 8-dim chain and publish every stage's zst
+ * rows as tagged granules; expansion workgroups (clip, 96 frames, 128 channels; one loader wave
+ * polls the stage rows into LDS while seven waves write the previous stage) write z_q_is / z_q
+ * under the chain. Outputs, layouts and expressions as vrvq_rvq_encode, and equal to its three
+ * launches bit for bit. When a clip does not fit the resident grid (very long clips; see
+ * vrvq_rvq_fused_clips) or vrvq_rvq_path(1) is set, the chain and the expansion run as two
+ * stream-ordered launches over the same partials (zst rows through the workspace), with the same
+ * outputs. workspace: >= vrvq_rvq_workspace_part bytes, 16-byte aligned (eager fused calls hand
+ * off through the library's granule area; under stream capture the granules and the sync block
+ * live in the workspace, zeroed by captured memsets). Replaces models/quantize.py:353-365,
+ * 389-421 like vrvq_rvq_encode. */
+int vrvq_rvq_workspace_part(int batch, int frames, int nq, int ncode, long long* bytes);
+int vrvq_rvq_encode_part(const float* part, int batch, int dim, int frames, int nq, int ncode,
+                         int cdim, const float* b_in, const float* cb, const float* cbf,
+                         const float* c2, const float* w_out, const float* b_out,
+                         const float* mcol, const float* qb, const float* imp, float level,
+                         int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
+                         float* z_q, float* mask, void* workspace, long long workspace_bytes,
+                         vrvq_stream_t stream);
+/* Clips one rvq_pt_kernel launch holds resident (0: vrvq_rvq_encode_part takes its two-launch
+ * form). vrvq_rvq_debug_capacity: test hook capping that number (0 forces the two launches, a
+ * negative value removes the cap); returns the previous cap. */
+int vrvq_rvq_fused_clips(int frames, int nq, int ncode, int* clips);
+int vrvq_rvq_debug_capacity(int clips);
 
 /* The whole quantizer, the replacement of VBRResidualVectorQuantize.forward's quantizer loop,
  * importance mask and masked sum (models/quantize.py:353-365, 389-421) and of

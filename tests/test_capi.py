@@ -70,6 +70,19 @@ def test_argument_errors_raise_before_launch():
     assert n.value == (2 * 8 * 32 * 87 * 64 + max(32 * 87 * 8 * 8, 32 * 8 * 8 * 16 * 8 * 2)) * 4 \
         + sync
     assert lib.vrvq_rvq_path(7) == 10001 and lib.vrvq_rvq_path(0) in (1, 2)
+    # the quantizer from the conv's partials: the larger of the captured launch's stage granules
+    # (B nq ceil(87 / 16) parts x 16 frames x d x 8 B, + the sync block) and the two-launch
+    # fallback's zst rows
+    assert lib.vrvq_rvq_workspace_part(32, 87, 8, 1024, ctypes.byref(n)) == 0
+    assert n.value == max(32 * 8 * 6 * 16 * 8 * 8 + sync, 32 * 8 * 87 * 8 * 4)
+    assert lib.vrvq_rvq_workspace_part(32, 87, 33, 1024, ctypes.byref(n)) == 10002
+    assert lib.vrvq_rvq_encode_part(*([None] + [1] * 6 + [None] * 9 + [1.0] + [None] * 7 +
+                                      [0, None])) == 10001
+    assert lib.vrvq_conv1d_proj(None, 1, 1024, 87, None, None, None, None, 1024, 1024, 3, 1, 1,
+                                None, None, 87, None, 8, None, None) == 10001
+    # the projection epilogue serves the 1024-channel latent only
+    assert lib.vrvq_conv1d_proj(p16 := ctypes.c_void_p(16), 1, 512, 87, None, None, p16, None,
+                                512, 512, 3, 1, 1, None, None, 87, p16, 8, p16, None) == 10002
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
     # geometry mismatch (tout inconsistent with the conv formula)

@@ -53,6 +53,9 @@ def test_mpd_folded_gemm_matches_conv2d(monkeypatch):
         b, c, frames, p = r.shape
         got = a.reshape(b, p, frames, c).permute(0, 3, 2, 1)
         torch.testing.assert_close(got, r, rtol=1e-4, atol=1e-6)
+        # the documented converter gives the same view
+        assert torch.equal(mpd.to_reference_layout(a, b), got)
+        assert mpd.to_reference_layout(r, b) is r
 
 
 def test_stft_match_stride_frames():

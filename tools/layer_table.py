@@ -23,20 +23,23 @@ CALLS = []
 def _fake():
     def conv1d(x, wp, cout, cout_pad, k, stride=1, pad=0, dil=1, bias=None, alpha=None,
                inv_alpha=None, residual=None, epilogue=0, out_snake=None, want_raw=True,
-               w_x3=None, ys_planes=False):
-        if x.dim() == 5:  # planes input (B, 3, C/8, T, 8)
-            B, cin, tin = x.shape[0], x.shape[2] * 8, x.shape[3]
-        else:
-            B, cin, tin = x.shape
+               w_x3=None):
+        B, cin, tin = x.shape
         tout = (tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
         CALLS.append(("conv", cin, cout, k, stride, dil, tout, B,
                       2.0 * B * cout * tout * cin * k, residual is not None))
         y = torch.empty(B, cout, tout)
         if out_snake is None:
             return y
-        ys = torch.empty(B, 3, cout // 8, tout, 8, dtype=torch.int16) if ys_planes else \
-            torch.empty_like(y)
-        return y, ys
+        return y, torch.empty_like(y)
+
+    def conv1d_proj(x, wp, cout, k, w3in, nq, pad=0, dil=1, bias=None, alpha=None,
+                    inv_alpha=None, w_x3=None, want_z=False):
+        B, cin, tin = x.shape
+        tout = tin + 2 * pad - dil * (k - 1)
+        CALLS.append(("conv", cin, cout, k, 1, dil, tout, B, 2.0 * B * cout * tout * cin * k,
+                      False))
+        return torch.empty(8, B * tout, 8 * nq), (torch.empty(B, cout, tout) if want_z else None)
 
     def conv1d_fm(x, wp, cout, k, pad=0, dil=1, bias=None, alpha=None, inv_alpha=None,
                   w_x3=None):
@@ -47,16 +50,14 @@ def _fake():
         return torch.empty(B, tout, cout)
 
     def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None,
-              out_snake=None, want_raw=True, pad=-1, w_x3=None, ys_planes=False):
+              out_snake=None, want_raw=True, pad=-1, w_x3=None):
         B, cin, tin = x.shape
         CALLS.append(("convT", cin, cout, 2 * stride, stride, 1, tin * stride, B,
                       2.0 * B * cin * cout * tin * 2 * stride, False))
         y = torch.empty(B, cout, tin * stride)
         if out_snake is None:
             return y
-        ys = torch.empty(B, 3, cout // 8, tin * stride, 8, dtype=torch.int16) if ys_planes \
-            else torch.empty_like(y)
-        return y, ys
+        return y, torch.empty_like(y)
 
     def residual_unit(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, cout_pad,
                       out_snake=None, want_raw=True, w7_x3=None, w1_x3=None):
@@ -102,7 +103,17 @@ def _fake():
                 torch.empty(B, nq, T), torch.empty(B, nq, D, T) if want_z_q_is else None,
                 torch.empty(B, D, T), torch.empty(B, nq, T) if want_mask else None)
 
+    def rvq_encode_part(part, T, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None, level=1.0,
+                        want_z_q_is=True, want_mask=True):
+        B = part.shape[1] // T
+        nq, D = cb.shape[0], w_out.shape[1]
+        return (torch.zeros(B, nq, T, dtype=torch.long), torch.empty(B, nq * 8, T),
+                torch.empty(B, nq, T), torch.empty(B, nq, D, T) if want_z_q_is else None,
+                torch.empty(B, D, T), torch.empty(B, nq, T) if want_mask else None)
+
     ops.rvq_encode = rvq_encode
+    ops.rvq_encode_part = rvq_encode_part
+    ops.conv1d_proj = conv1d_proj
     ops.conv1d_fm = conv1d_fm
     ops.rvq_pack_w_in = lambda w: w
     ops.rvq_encode_fm = lambda zt, w3in, *a, **k: rvq_encode(zt.transpose(1, 2), None, *a, **k)
@@ -130,7 +141,7 @@ def main():
     rows = list(csv.DictReader(open(args.trace)))
     conv = [r for r in rows if any(k in r["Kernel_Name"] for k in
                                    ("conv_mfma_kernel", "conv_small", "conv_cout1", "conv_cin1",
-                                    "ru_fused_kernel", "conv_pl_kernel"))]
+                                    "ru_fused_kernel"))]
     step = conv[-len(CALLS):]
     tot_t = tot_f = 0.0
     # %pk against the ceiling of the path the kernel runs: the x3 split-bf16 MFMA (template
@@ -141,11 +152,10 @@ def main():
         kn = r["Kernel_Name"]
         i = kn.find("<")
         pre = ("mfma" if "mfma" in kn else "ru" if "ru_fused" in kn else
-               "planes" if "conv_pl_kernel" in kn else
                "cout1" if "cout1" in kn else "cin1" if "cin1" in kn else "small")
         targs = [t.strip() for t in kn[i + 1:kn.find(">")].split(",")] if i >= 0 else []
         # conv_mfma_kernel<BM, BN, WM, NW, KS, X3[, PH]>, ru_fused_kernel<C, BN, WM, NW, X3>
-        x3 = (pre == "planes" or (pre == "mfma" and len(targs) >= 6 and targs[5] == "true") or
+        x3 = ((pre == "mfma" and len(targs) >= 6 and targs[5] == "true") or
               (pre == "ru" and len(targs) >= 5 and targs[4] == "true"))
         kn = pre + kn[i:kn.find(">") + 1] if i >= 0 else pre
         tf = c[8] / (us * 1e-6) / 1e12

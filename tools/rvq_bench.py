@@ -15,9 +15,13 @@ from vrvq_amd import ops  # noqa: E402
 from vrvq_amd.recipe import load_recipe  # noqa: E402
 
 
-def rvq_bytes(B, T, nq, D=1024, d=8, N=1024):
-    per_frame = D * 4 + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
-    return B * T * per_frame + nq * 4 * (d * D + d + 2 * N * d + D * d + D)
+def rvq_bytes(B, T, nq, D=1024, d=8, N=1024, from_partials=False):
+    """bench.py's count: SURVEY §8(d); from_partials (path pt) reads the 8 channel-split in_proj
+    partials instead of z, and not W_in."""
+    inp = 8 * nq * d * 4 if from_partials else D * 4
+    per_frame = inp + 4 + nq * D * 4 + D * 4 + nq * 8 + nq * d * 4 + nq * 4 + nq * 4
+    return B * T * per_frame + nq * 4 * ((0 if from_partials else d * D) + d + 2 * N * d +
+                                         D * d + D)
 
 
 def main():
@@ -28,9 +32,10 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
     ap.add_argument("--variants", default="3,2", help="projection kernel variants to time (1,2,3)")
-    ap.add_argument("--paths", default="fm,2,1",
-                    help="RVQ launch structures to time (fm: frame-major fused launch, 2 fused, "
-                         "1 three launches)")
+    ap.add_argument("--paths", default="pt,fm,2,1",
+                    help="RVQ launch structures to time (pt: the launch from the conv's projection "
+                         "partials, the eval encode's; fm: frame-major fused launch, 2 fused, 1 "
+                         "three launches)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -49,15 +54,26 @@ def main():
                                        st.b_out, st.mcol, st.qb, imp=imp, level=1.0,
                                        want_z_q_is=not args.no_zqis)
     from vrvq_amd import _lib
+    part = torch.empty(8, args.batch * args.frames, args.nq * 8, device=dev)
+    import ctypes
+    _lib.call("vrvq_rvq_project", ctypes.c_void_p(z.data_ptr()), args.batch, 1024, args.frames,
+              args.nq, 8, ctypes.c_void_p(st.w_in_t.data_ptr()), ctypes.c_void_p(part.data_ptr()),
+              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    run_pt = lambda: ops.rvq_encode_part(part, args.frames, st.b_in, st.cb, st.cbf, st.c2,  # noqa: E731
+                                         st.w_out, st.b_out, st.mcol, st.qb, imp=imp, level=1.0,
+                                         want_z_q_is=not args.no_zqis)
     runs = []
     for p in args.paths.split(","):
-        if p == "fm":
-            runs.append(("fm", 0))
+        if p in ("fm", "pt"):
+            runs.append((p, 0))
         else:
             runs += [(int(p), int(x)) for x in args.variants.split(",")]
     for path, v in runs:
         if path == "fm":
             run = run_fm
+        elif path == "pt":
+            run = run_pt
+            _lib.rvq_path(2)  # (a numeric path left at 1 would select pt's two-launch form)
         else:
             run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
                                          want_z_q_is=not args.no_zqis)
@@ -88,7 +104,7 @@ def main():
         torch.cuda.synchronize()
         kms, kn = _lib.rvq_timing_read()
         _lib.rvq_timing(False)
-        byt = rvq_bytes(args.batch, args.frames, args.nq)
+        byt = rvq_bytes(args.batch, args.frames, args.nq, from_partials=path == "pt")
         tag = "rvq_encode no z_q_is" if args.no_zqis else "rvq_encode"
         print(f"path {path} projection v{v} B={args.batch} nq={args.nq} T={args.frames}: {tag} median "
               f"{med:.1f} us (min {min(ts):.1f}), {byt / med / 1e3:.0f} GB/s algorithmic "

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--fm", action="store_true",
                     help="the frame-major launch (vrvq_rvq_encode_fm: chain parts project their "
                          "own frames)")
+    ap.add_argument("--pt", action="store_true",
+                    help="the launch from the conv's projection partials (vrvq_rvq_encode_part: "
+                         "rvq_pt_kernel; partials made here by vrvq_rvq_project)")
     ap.add_argument("--flags", type=int, default=0,
                     help="timing experiment: vrvq_debug_set_fused_flags bits (2: the chain parts "
                          "skip the next stage's codebook fragment loads; outputs not checked)")
@@ -71,8 +74,30 @@ def main():
     w3in = st.w3in()
     assert T <= 128, "the frame-major timeline assumes 8 chain parts per clip"
 
+    if args.pt:
+        part = torch.empty(8, B * T, nq * 8, device=dev)
+        assert lib.vrvq_rvq_project(P(z), B, 1024, T, nq, 8, P(st.w_in_t), P(part), stream) == 0
+        n2 = ctypes.c_longlong(0)
+        assert lib.vrvq_rvq_workspace_part(B, T, nq, 1024, ctypes.byref(n2)) == 0
+        wsp = torch.empty((n2.value + 3) // 4, device=dev)
+        F_env = int(os.environ.get("VRVQ_RVQ_PT_F", "0"))
+        F = min(F_env, T) if 1 <= F_env <= 16 else ((T + 7) // 8 if T <= 128 else 16)
+        P_parts = (T + F - 1) // F
+        n_fb = (T + 95) // 96
+        grid = B * (P_parts + 8 * n_fb)
+        stamps = torch.zeros(grid * 64, dtype=torch.int64, device=dev)
+
     def run(with_stamps):
         lib.vrvq_debug_set_fused_stamps(P(stamps) if with_stamps else None)
+        if args.pt:
+            rc = lib.vrvq_rvq_encode_part(P(part), B, 1024, T, nq, 1024, 8, P(st.b_in), P(st.cb),
+                                          P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
+                                          P(st.mcol), P(st.qb), P(imp), ctypes.c_float(1.0),
+                                          P(codes), P(lat), P(loss),
+                                          None if args.no_zqis else P(zqis), P(zq), P(mask),
+                                          P(wsp), ctypes.c_longlong(wsp.numel() * 4), stream)
+            assert rc == 0, rc
+            return
         if args.fm:
             rc = lib.vrvq_rvq_encode_fm(P(zt), B, 1024, T, nq, 1024, 8, P(w3in), P(st.b_in),
                                         P(st.cb), P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
@@ -104,7 +129,10 @@ def main():
         lib.vrvq_debug_set_fused_flags(0)
         print(f"fused flags {flags} (timing experiment: 1 expansion MFMAs skipped, 2 chain "
               "codebook stream skipped)")
-    if args.fm:
+    if args.pt:
+        ref = vrvq_amd.ops.rvq_encode_part(part, T, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
+                                           st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
+    elif args.fm:
         ref = vrvq_amd.ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
                                          st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
     else:
@@ -119,20 +147,22 @@ def main():
     s = stamps.cpu().numpy().reshape(grid, 64).astype(np.int64)
     t0 = s[:, 0].min()
     us = lambda v: (v - t0) / 100.0  # noqa: E731
-    pc, ex = s[: B * 8], s[B * 8:]
+    npc = B * (P_parts if args.pt else 8)
+    pc, ex = s[:npc], s[npc:]
 
     def row(name, v):
         v = us(v)
         print(f"  {name:34s} median {np.median(v):7.2f}  max {v.max():7.2f}  min {v.min():7.2f}")
 
-    print(f"B={B} nq={nq} T={T}: {B * 8} projection/chain + {B * 8} expansion workgroups (us)")
+    print(f"B={B} nq={nq} T={T}: {len(pc)} chain + {len(ex)} expansion workgroups (us)")
     print("projection / chain workgroups")
     row("start", pc[:, 0])
-    row("z slab in LDS" if not args.fm else "K-half 0 staged", pc[:, 44])
-    if args.fm:
-        row("K-half 1 staged", pc[:, 46])
-    row("projection MFMAs + stores issued", pc[:, 45])
-    if not args.fm:
+    if not args.pt:
+        row("z slab in LDS" if not args.fm else "K-half 0 staged", pc[:, 44])
+        if args.fm:
+            row("K-half 1 staged", pc[:, 46])
+        row("projection MFMAs + stores issued", pc[:, 45])
+    if not args.fm and not args.pt:
         row("clip's partials seen (thread 0)", pc[:, 2])
     row("prologue done", pc[:, 3])
     for i in range(nq):
@@ -142,7 +172,7 @@ def main():
     row("start", ex[:, 0])
     for i in range(nq):
         if i < 8:
-            row(f"stage {i} slice seen (thread 0)", ex[:, 56 + i])
+            row(f"stage {i} slice seen ({'loader' if args.pt else 'thread 0'})", ex[:, 56 + i])
         row(f"stage {i} start", ex[:, 1 + i])
         if i < 8:
             row(f"stage {i} stores issued (thread 0)", ex[:, 48 + i])

@@ -8,8 +8,8 @@ from .model import (DAC_VRVQ, Decoder, Encoder, ImportanceSubnet, ResidualVector
                     VBRResidualVectorQuantize, VectorQuantize)
 from .layers import (DecoderBlock, EncoderBlock, ResidualUnit, Snake1d, WNConv1d,
                      WNConvTranspose1d)
-from .utils import (cal_bpf_from_mask, cal_bpf_tensor, generate_mask_hard, generate_mask_ste,
-                    level_sweep, masked_sum, scale_importance)
+from .utils import (cal_bpf_from_mask, cal_bpf_tensor, check_errors, generate_mask_hard,
+                    generate_mask_ste, level_sweep, masked_sum, scale_importance)
 from .config import from_config, load_config, model_kwargs
 
 __all__ = [
@@ -18,5 +18,5 @@ __all__ = [
     "WNConvTranspose1d", "ResidualUnit", "EncoderBlock", "DecoderBlock",
     "generate_mask_hard", "generate_mask_ste", "cal_bpf_from_mask", "cal_bpf_tensor",
     "masked_sum", "scale_importance", "level_sweep", "load_config", "model_kwargs",
-    "from_config",
+    "from_config", "check_errors",
 ]

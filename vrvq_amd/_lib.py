@@ -26,11 +26,9 @@ SIGNATURES = {
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
-    "vrvq_conv1d_ex": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I,
-                       _P, _I, _P, _P, _P, _P, _P],
-    "vrvq_conv_transpose1d_ex": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
-                                 _P, _P, _P],
     "vrvq_conv1d_fm": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
+    "vrvq_conv1d_proj": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
+                         _P, _P],
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
     "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],
@@ -50,6 +48,10 @@ SIGNATURES = {
     "vrvq_rvq_workspace_fm": [_I, _I, _I, _I, _P],
     "vrvq_rvq_encode_fm": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                            _F, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
+    "vrvq_rvq_workspace_part": [_I, _I, _I, _I, _P],
+    "vrvq_rvq_encode_part": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
+                             _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
+    "vrvq_rvq_fused_clips": [_I, _I, _I, _P],
     "vrvq_rvq_project": [_P, _I, _I, _I, _I, _I, _P, _P, _P],
     "vrvq_rvq_chain": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P,
                        _P],
@@ -87,7 +89,8 @@ EXTRA = {"vrvq_status_string": ([_I], ctypes.c_char_p), "vrvq_version": ([], _I)
          "vrvq_rvq_project_variant": ([_I], _I), "vrvq_rvq_path": ([_I], _I),
          "vrvq_rvq_sync_error": ([_P, _P], _I), "vrvq_rvq_timing": ([_I], _I),
          "vrvq_rvq_timing_read": ([_P, _P], _I), "vrvq_rvq_pending_error": ([_P], _I),
-         "vrvq_rvq_debug": ([ctypes.c_uint, ctypes.c_uint], _I)}
+         "vrvq_rvq_debug": ([ctypes.c_uint, ctypes.c_uint], _I),
+         "vrvq_rvq_debug_capacity": ([_I], _I)}
 
 _lock = threading.Lock()
 _lib = None
@@ -155,6 +158,20 @@ def rvq_debug(spin_max: int = 0, stall: int = 0) -> None:
     """Test hook: bound every later fused launch's waits at spin_max polls (0: default) and delay
     its first chain part by stall x s_sleep(127)."""
     call("vrvq_rvq_debug", ctypes.c_uint(spin_max), ctypes.c_uint(stall))
+
+
+def rvq_fused_clips(frames: int, nq: int, ncode: int = 1024) -> int:
+    """Clips one fused launch from the conv's partials holds resident (0: the two-launch form
+    runs; include/vrvq.h vrvq_rvq_fused_clips)."""
+    n = ctypes.c_int(0)
+    call("vrvq_rvq_fused_clips", frames, nq, ncode, ctypes.byref(n))
+    return n.value
+
+
+def rvq_debug_capacity(clips: int) -> int:
+    """Test hook: cap the clips per fused launch from partials (0 forces the two launches, -1
+    removes the cap). Returns the previous cap."""
+    return int(load().vrvq_rvq_debug_capacity(int(clips)))
 
 
 def rvq_timing(on: bool) -> bool:

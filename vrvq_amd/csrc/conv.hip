@@ -17,7 +17,6 @@
 #include "common.h"
 #include "conv_core.h"
 #include "conv_x3.h"
-#include "conv_pl.h"
 #include <stdlib.h>
 
 namespace {
@@ -64,46 +63,6 @@ void conv_mfma_kernel(ConvArgs a) {
   if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
   else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
-}
-
-// The planes k7 tile (conv_pl.h): x = snake(x) as bf16 planes, both operands by LDS-DMA, one
-// workgroup per CU; the epilogue is every conv's (y / planes of the next Snake / residual).
-__global__ __launch_bounds__(64 * PL_NW) void conv_pl_kernel(ConvArgs a) {
-  using TC = TileCfg<PL_BM, PL_BN, 1, PL_NW>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  int bid = blockIdx.x;
-  const int mt = bid % a.n_mt;
-  bid /= a.n_mt;
-  const int nt = bid % a.n_nt;
-  const int b = bid / a.n_nt;
-  const int m0 = mt * PL_BM, n0 = nt * PL_BN;
-  f32x16 acc[TC::RM][TC::RN];
-#pragma unroll
-  for (int i = 0; i < TC::RM; ++i)
-#pragma unroll
-    for (int j = 0; j < TC::RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  conv_mainloop_pl<PL_BM, PL_BN, 1, PL_NW>(a, smem, acc, b, m0, n0);
-  __syncthreads();
-  conv_epilogue<PL_BM, PL_BN, 1, PL_NW>(a, smem, acc, b, m0, n0);
-}
-
-int launch_pl(const ConvArgs& a0, int batch, hipStream_t st) {
-  ConvArgs a = a0;
-  a.n_mt = (a.M + PL_BM - 1) / PL_BM;
-  a.n_nt = (a.ng + PL_BN - 1) / PL_BN;
-  if (a.m_pad < a.n_mt * PL_BM) return VRVQ_ERR_ARG;
-  const long long nblk = (long long)a.n_mt * a.n_nt * batch;
-  if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
-  size_t lds = PL_LDS;
-  const size_t epi = (size_t)PL_BM * EpiCfg<PL_BM, PL_BN, PL_NW>::BNP * sizeof(float);
-  if (lds < epi) lds = epi;
-  hipError_t e = hipFuncSetAttribute((const void*)conv_pl_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(conv_pl_kernel, dim3((unsigned)nblk), dim3(64 * PL_NW), lds, st, a);
-  return vrvq_launch_status();
 }
 
 // Small-Cout conv (Cout <= 8, stride 1): the decoder's 96->1 k7 + Tanh output layer and the
@@ -454,7 +413,11 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   const int XW = (BN - 1) * a.stride + (KS - 1) * a.dil + 1;
   const int XP = a.ssh ? (XW + a.stride - 1) >> a.ssh : XW;
   const int XWP = a.ssh ? ((XP << a.ssh) + 3) & ~3 : (XW + 3) & ~3;
-  const size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
+  size_t epi = (size_t)BM * EpiCfg<BM, BN, NW / WM>::BNP * sizeof(float);
+  if (a.pj_part) {  // RVQ in_proj epilogue: one latent split per tile, its z planes in LDS
+    if (BM != 128) return VRVQ_ERR_UNSUPPORTED;
+    if (epi < (size_t)PJE_LDS) epi = PJE_LDS;
+  }
   const long long nblk = (long long)a.n_mt * a.n_nt * batch;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
   // bf16x3 split path (conv_x3.h): stride-1 windows, a pre-split weight, the stage in LDS
@@ -818,22 +781,8 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
                            const float* residual, int epilogue, float* y, int tout,
                            const float* alpha_out, const float* inv_alpha_out, float* y_snake,
                            vrvq_stream_t stream) {
-  return vrvq_conv1d_ex(x, 0, batch, cin, tin, alpha, inv_alpha, w_packed, w_x3, cout, cout_pad,
-                        k, stride, pad, dil, bias, residual, epilogue, y, tout, alpha_out,
-                        inv_alpha_out, y_snake, nullptr, stream);
-}
-
-extern "C" int vrvq_conv1d_ex(const void* x, int x_planes, int batch, int cin, int tin,
-                              const float* alpha, const float* inv_alpha, const float* w_packed,
-                              const uint16_t* w_x3, int cout, int cout_pad, int k, int stride,
-                              int pad, int dil, const float* bias, const float* residual,
-                              int epilogue, float* y, int tout, const float* alpha_out,
-                              const float* inv_alpha_out, float* y_snake,
-                              uint16_t* y_snake_planes, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake || y_snake_planes));
-  VRVQ_CHECK_ARG(!(y_snake && y_snake_planes));
-  VRVQ_CHECK_ARG((y_snake == nullptr && y_snake_planes == nullptr) || (alpha_out && inv_alpha_out));
-  VRVQ_CHECK_ARG(y_snake_planes == nullptr || (cout % 8 == 0 && ((uintptr_t)y_snake_planes & 15) == 0));
+  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
+  VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && stride > 0 &&
                  dil > 0 && pad >= 0 && tout > 0);
   VRVQ_CHECK_ARG(cout_pad >= cout && cout_pad % 128 == 0);
@@ -842,25 +791,12 @@ extern "C" int vrvq_conv1d_ex(const void* x, int x_planes, int batch, int cin, i
   const long long expect = ((long long)tin + 2LL * pad - (long long)dil * (k - 1) - 1) / stride + 1;
   VRVQ_CHECK_ARG(expect == tout);
   ConvArgs a{};
-  a.x = static_cast<const float*>(x); a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed;
+  a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed;
   a.bias = bias; a.res = residual; a.y = y;
   a.alpha_o = alpha_out; a.inv_alpha_o = inv_alpha_out; a.ys = y_snake;
-  a.ysp = reinterpret_cast<unsigned short*>(y_snake_planes);
   a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
   a.stride = stride; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0;
   a.ssh = 0;
-  if (x_planes) {
-    // x holds snake(x) as bf16 planes [B][3][cin / 8][tin][8] (a planes epilogue wrote them):
-    // the k7 planes tile, the only consumer of that layout
-    if (k != 7 || stride != 1 || alpha || !w_x3 || cin % 16 != 0 || cout % 64 != 0 ||
-        cout < 128 || dil > 9 || pad != 3 * dil)
-      return VRVQ_ERR_UNSUPPORTED;
-    VRVQ_CHECK_ARG(((uintptr_t)x & 15) == 0);
-    a.w3 = reinterpret_cast<const unsigned*>(w_x3);
-    a.ylen = tout; a.epi = epilogue;
-    return launch_pl(a, batch, as_stream(stream));
-  }
-  if (y_snake_planes && (cout <= SMALL_COUT || cin == 1)) return VRVQ_ERR_UNSUPPORTED;
   if (stride > 1 && (stride & (stride - 1)) == 0)
     while ((1 << a.ssh) < stride) ++a.ssh;
   a.ylen = tout; a.epi = epilogue;
@@ -912,6 +848,36 @@ extern "C" int vrvq_conv1d_fm(const float* x, int batch, int cin, int tin, const
   return dispatch_ks(k, a, batch, as_stream(stream));
 }
 
+extern "C" int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, const float* alpha,
+                                const float* inv_alpha, const float* w_packed,
+                                const uint16_t* w_x3, int cout, int cout_pad, int k, int pad,
+                                int dil, const float* bias, float* y, int tout,
+                                const uint16_t* w3in, int nq, float* part,
+                                vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(x && w_packed && w3in && part);
+  VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && dil > 0 && pad >= 0 &&
+                 tout > 0 && nq > 0);
+  VRVQ_CHECK_ARG(cout_pad >= cout && cout_pad % 128 == 0);
+  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
+  VRVQ_CHECK_ARG(((uintptr_t)part & 15) == 0 && ((uintptr_t)w3in & 15) == 0);
+  if (cout != 1024 || nq > 32) return VRVQ_ERR_UNSUPPORTED;  // the latent (RD) / CH_NQMAX
+  const long long expect = (long long)tin + 2LL * pad - (long long)dil * (k - 1);
+  VRVQ_CHECK_ARG(expect == tout);
+  VRVQ_CHECK_ARG((long long)batch * tout * nq * 8 * 8 < 0x7fffffffLL);
+  ConvArgs a{};
+  a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias; a.y = y;
+  a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
+  a.stride = 1; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0; a.ssh = 0;
+  a.ylen = tout; a.epi = VRVQ_EPI_NONE;
+  a.w3 = reinterpret_cast<const unsigned*>(w_x3);
+  a.pj_w3 = reinterpret_cast<const unsigned*>(w3in);
+  a.pj_part = part;
+  a.pj_nq = nq;
+  a.pj_nf = batch * tout;
+  // the MFMA tiles only (their epilogue owns the projection); every 1024-row tile is 128 rows
+  return dispatch_ks(k, a, batch, as_stream(stream));
+}
+
 extern "C" int vrvq_conv_transpose1d(const float* x, int batch, int cin, int tin,
                                      const float* alpha, const float* inv_alpha,
                                      const float* w_packed, int cout, int cout_pad, int stride,
@@ -931,24 +897,8 @@ extern "C" int vrvq_conv_transpose1d_pad(const float* x, int batch, int cin, int
                                          int stride, int pad, const float* bias, float* y,
                                          const float* alpha_out, const float* inv_alpha_out,
                                          float* y_snake, vrvq_stream_t stream) {
-  return vrvq_conv_transpose1d_ex(x, batch, cin, tin, alpha, inv_alpha, w_packed, w_x3, cout,
-                                  cout_pad, stride, pad, bias, y, alpha_out, inv_alpha_out,
-                                  y_snake, nullptr, stream);
-}
-
-extern "C" int vrvq_conv_transpose1d_ex(const float* x, int batch, int cin, int tin,
-                                        const float* alpha, const float* inv_alpha,
-                                        const float* w_packed, const uint16_t* w_x3, int cout,
-                                        int cout_pad, int stride, int pad, const float* bias,
-                                        float* y, const float* alpha_out,
-                                        const float* inv_alpha_out, float* y_snake,
-                                        uint16_t* y_snake_planes, vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake || y_snake_planes));
-  VRVQ_CHECK_ARG(!(y_snake && y_snake_planes));
-  VRVQ_CHECK_ARG((y_snake == nullptr && y_snake_planes == nullptr) || (alpha_out && inv_alpha_out));
-  VRVQ_CHECK_ARG(y_snake_planes == nullptr ||
-                 (cout % 8 == 0 && (stride == 2 || stride == 4 || stride == 8) &&
-                  ((uintptr_t)y_snake_planes & 15) == 0));
+  VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
+  VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && stride > 0);
   // pad 0 = the padding=False windows of the chunked codec (models/dac_base.py:72-82)
   VRVQ_CHECK_ARG(pad >= 0 && pad < stride);
@@ -959,7 +909,6 @@ extern "C" int vrvq_conv_transpose1d_ex(const float* x, int batch, int cin, int 
   a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
   a.res = nullptr; a.y = y;
   a.alpha_o = alpha_out; a.inv_alpha_o = inv_alpha_out; a.ys = y_snake;
-  a.ysp = reinterpret_cast<unsigned short*>(y_snake_planes);
   a.cin = cin; a.tin = tin; a.M = cout * stride; a.m_pad = cout_pad; a.cout = cout;
   a.stride = 1; a.pad = 1; a.dil = 1; a.ng = tin + 1; a.up = stride; a.up_pad = p;
   a.ylen = (tin - 1) * stride - 2 * p + 2 * stride;

@@ -40,10 +40,13 @@ struct ConvArgs {
   // Frame-major output yfm[B][ng][M] (y of the encoder's last conv as the RVQ's zt,
   // vrvq_conv1d_fm): written straight from the accumulators with the bias, instead of y.
   float* yfm;
-  // snake_o(y) as three bf16 planes ysp[B][3][cout / 8][ylen][8] (v = h + m + l exactly, the
-  // split the x3 staging would make of the same fp32 value) instead of fp32 ys: the operand of
-  // the planes k7 tile (conv_pl.h), which fills its LDS stages with LDS-DMA, no VALU.
-  unsigned short* ysp;
+  // in_proj of every RVQ stage in the epilogue (vrvq_conv1d_proj, 128-row tiles of the
+  // 1024-channel z): pj_part[s][b * ng + n][8 pj_nq] over the tile's channel split s = m0 / 128,
+  // W_in as bf16 planes in the 16x16x32 A-fragment order (vrvq_rvq_pack_w_in); null: none
+  const unsigned* pj_w3;
+  float* pj_part;
+  int pj_nq;
+  int pj_nf;               // frames of the whole call (B * ng): the partials' split stride
 };
 
 // v = h + m + l exactly (RNE at each step; conv_x3.h split3x2), two values per call
@@ -61,18 +64,6 @@ __device__ __forceinline__ void split3x2_core(float v0, float v1, unsigned& h, u
   h = hu;
   m = mu;
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2_));
-}
-
-// Eight channels' snake values at one position -> their 16-B groups of the three planes.
-__device__ __forceinline__ void store_planes8(unsigned short* ysp, size_t plane_stride,
-                                              size_t off, const float (&v)[8]) {
-  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-  unsigned h[4], m[4], l[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) split3x2_core(v[2 * u], v[2 * u + 1], h[u], m[u], l[u]);
-  *reinterpret_cast<u32x4_*>(ysp + off) = u32x4_{h[0], h[1], h[2], h[3]};
-  *reinterpret_cast<u32x4_*>(ysp + plane_stride + off) = u32x4_{m[0], m[1], m[2], m[3]};
-  *reinterpret_cast<u32x4_*>(ysp + 2 * plane_stride + off) = u32x4_{l[0], l[1], l[2], l[3]};
 }
 
 template <int KS, int BM, int BN>
@@ -301,6 +292,110 @@ __device__ __forceinline__ void conv_mainloop(
 
 }
 
+// ---- in_proj of the RVQ stages in the epilogue of the encoder's last conv (vrvq_conv1d_proj).
+// For the tile's 128 output channels (latent split s = m0 / 128) and its frames:
+//   part[s][b * ng + n][r] = sum_{c in split s} W_in[r][c] z[c][n],  z = acc + bias,  r < 8 nq
+// -- rvq_project3_kernel's unit (csrc/rvq.hip, project3_body) bit for bit: z and W_in split
+// exactly into three bf16 planes; per 16-row x 16-frame tile the split's four 32-channel k-steps
+// in order, each k-step's six products m m, h l, l h, h m, m h, h h on v_mfma_f32_16x16x32_bf16
+// from a zero accumulator (each output column depends on its own frame only, so the tile width
+// does not change a bit). The chain then sums the eight splits in order, as the three-launch
+// path does: the quantizer's input never goes back to HBM as z and is not re-read from it.
+// z crosses LDS as three planes [plane][frame][channel] (rows of 128 + 8 channels: conflict-free
+// 16-B B reads), 32 frames per pass.
+constexpr int PJE_LDB = 136;                      // bf16 per frame row
+constexpr int PJE_FR = 32;                        // frames per pass
+constexpr int PJE_PLANE = PJE_FR * PJE_LDB * 2;   // bytes per plane (8,704)
+constexpr int PJE_LDS = 3 * PJE_PLANE;            // 26,112 B
+
+template <int BM, int BN, int WM, int NW>
+__device__ __forceinline__ void proj_epilogue(
+    const ConvArgs& a, float* smem,
+    const f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b,
+    int m0, int n0) {
+  static_assert(BM == 128, "one latent split (128 channels) per tile");
+  typedef unsigned pj_u32x4 __attribute__((ext_vector_type(4)));
+  typedef float pj_f32x4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 pj_bf16x8 __attribute__((ext_vector_type(8)));
+  using TC = TileCfg<BM, BN, WM, NW>;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int fr = lane & 15, kg = lane >> 4;  // 16x16x32 roles: frame / row, k group
+  const int s = m0 / BM;
+  const int R = a.pj_nq * 8, n_rt = (R + 15) / 16;
+  const pj_u32x4* w3 = reinterpret_cast<const pj_u32x4*>(a.pj_w3);
+  char* lds = reinterpret_cast<char*>(smem);
+  auto mfma = [](pj_u32x4 x, pj_u32x4 y, pj_f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pj_bf16x8, x),
+                                                   __builtin_bit_cast(pj_bf16x8, y), c, 0, 0, 0);
+  };
+  // A planes of one item (row tile rt): the split's 4 k-steps x 3 planes, L2 -> registers
+  auto load_a = [&](int rt, pj_u32x4 (&av)[4][3]) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        av[kk][p] = w3[((size_t)((4 * s + kk) * 3 + p) * n_rt + rt) * 64 + lane];
+  };
+  const int n_items = 2 * n_rt;  // (row tile, 16-frame half of the pass)
+  for (int p0 = 0; p0 < BN; p0 += PJE_FR) {
+    if (n0 + p0 >= a.ng) break;  // block-uniform
+    pj_u32x4 av[4][3];
+    if (wave < n_items) load_a(wave >> 1, av);  // the first item's weights under the staging
+    __syncthreads();  // the previous pass's planes are no longer read
+    // z of this pass's 32 columns (one 32-column accumulator block of one wave column) -> planes
+#pragma unroll
+    for (int j = 0; j < TC::RN; ++j) {
+      if (wn * TC::TN + j * 32 != p0) continue;
+#pragma unroll
+      for (int i = 0; i < TC::RM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ml = wm * TC::TM + i * 32 + 8 * q + 4 * lh;  // channels ml .. ml + 3
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            v[u] = a.bias ? acc[i][j][4 * q + u] + a.bias[m0 + ml + u] : acc[i][j][4 * q + u];
+          unsigned h[2], mm[2], l[2];
+          split3x2_core(v[0], v[1], h[0], mm[0], l[0]);
+          split3x2_core(v[2], v[3], h[1], mm[1], l[1]);
+          char* d = lds + lr * (PJE_LDB * 2) + ml * 2;
+          *reinterpret_cast<uint2*>(d) = make_uint2(h[0], h[1]);
+          *reinterpret_cast<uint2*>(d + PJE_PLANE) = make_uint2(mm[0], mm[1]);
+          *reinterpret_cast<uint2*>(d + 2 * PJE_PLANE) = make_uint2(l[0], l[1]);
+        }
+    }
+    __syncthreads();
+    for (int it = wave; it < n_items; it += NW) {
+      const int rt = it >> 1, ct = it & 1;
+      if (it != wave) load_a(rt, av);
+      pj_f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const char* bp = lds + (ct * 16 + fr) * (PJE_LDB * 2) + (32 * kk + 8 * kg) * 2;
+        const pj_u32x4 bh = *reinterpret_cast<const pj_u32x4*>(bp);
+        const pj_u32x4 bm = *reinterpret_cast<const pj_u32x4*>(bp + PJE_PLANE);
+        const pj_u32x4 bl = *reinterpret_cast<const pj_u32x4*>(bp + 2 * PJE_PLANE);
+        d4 = mfma(av[kk][1], bm, d4);  // m m
+        d4 = mfma(av[kk][0], bl, d4);  // h l
+        d4 = mfma(av[kk][2], bh, d4);  // l h
+        d4 = mfma(av[kk][0], bm, d4);  // h m
+        d4 = mfma(av[kk][1], bh, d4);  // m h
+        d4 = mfma(av[kk][0], bh, d4);  // h h
+      }
+      // D: lane l, reg q -> row 16 rt + 4 (l >> 4) + q, frame l & 15
+      const int rr = rt * 16 + 4 * kg;  // rows rr .. rr + 3 all valid iff rr < R (R = 8 nq)
+      const int n = n0 + p0 + ct * 16 + fr;
+      if (rr < R && n < a.ng)
+        *reinterpret_cast<float4*>(a.pj_part + ((size_t)s * a.pj_nf + (size_t)b * a.ng + n) * R + rr) =
+            make_float4(d4[0], d4[1], d4[2], d4[3]);
+    }
+  }
+  __syncthreads();  // every LDS buffer free again for the epilogue below
+}
+
 // Epilogue through LDS: the accumulator tile is transposed to row-major [BM][BNP] so each wave
 // stores 64 consecutive output positions of one row (bias, residual, Tanh/Sigmoid, y and the
 // next layer's Snake). Expects every LDS buffer free (after a barrier).
@@ -325,6 +420,12 @@ __device__ __forceinline__ void conv_epilogue(
   const int lr = lane & 31;
   const int lh = lane >> 5;
 
+  if constexpr (BM == 128) {
+    if (a.pj_part) {
+      proj_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
+      if (!a.yfm && !a.y && !a.ys) return;  // z itself not wanted: the partials are its use
+    }
+  }
   if (a.yfm) {
     // frame-major: lane (col, lh) holds rows 8 q + 4 lh + (0..3) of column col for q = 0..3 --
     // one 16-B store per (tile, q), the two lane halves' 16 B adjacent (32-B runs per column;
@@ -374,34 +475,7 @@ __device__ __forceinline__ void conv_epilogue(
     }
     __syncthreads();
     const int p0 = n0 + pass * BNP;  // first GEMM column of this pass
-    if (a.up == 0 && a.ysp) {
-      // planes output: item = (channel octet, column); per item the eight rows' conv_epilogue
-      // expressions (bias, residual, act, y) and snake_o, then the 16-B groups of the planes.
-      // Consecutive lanes take consecutive columns: every plane store is 1 KB per wave.
-      const int ncols = min(BNP, a.ng - p0);
-      const int nocts = mrows >> 3;  // M % 8 == 0 (the launcher checks)
-      const size_t pstride = (size_t)(a.cout >> 3) * a.ylen * 8;  // bf16 per plane
-      for (int e = tid; e < nocts * BNP; e += NT) {
-        const int o = e / BNP, nl = e - o * BNP;
-        if (nl >= ncols) continue;
-        const int n = p0 + nl;
-        float v[8], al[8], ia[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int m = m0 + 8 * o + u;
-          v[u] = ct[(8 * o + u) * BNP + nl] + (a.bias ? a.bias[m] : 0.0f);
-          const size_t ob = ((size_t)b * a.cout + m) * a.ylen + n;
-          if (a.res) v[u] = a.res[ob] + v[u];
-          v[u] = apply_epi(v[u], a.epi);
-          if (a.y) a.y[ob] = v[u];
-          al[u] = a.alpha_o[m];
-          ia[u] = a.inv_alpha_o[m];
-        }
-        snake_n<8>(v, al, ia);
-        const size_t off = ((((size_t)b * 3) * (a.cout >> 3) + ((m0 >> 3) + o)) * a.ylen + n) * 8;
-        store_planes8(a.ysp, pstride, off, v);
-      }
-    } else if (a.up == 0) {
+    if (a.up == 0) {
       // Each thread owns 4 consecutive columns per step; U steps are loaded (accumulator
       // tile, bias, residual, next-layer alpha) before anything is stored, so the global
       // loads of a step group are in flight together.
@@ -531,39 +605,7 @@ __device__ __forceinline__ void conv_epilogue(
           }
         }
       };
-      // planes output (snake_o(y) for a planes k7 consumer): item = (channel octet, output
-      // sample), the walk4 expressions per channel, consecutive lanes on consecutive samples
-      auto walk_planes = [&](auto up_c) {
-        constexpr int UP = decltype(up_c)::value;
-        const int co0 = m0 / UP, nco = min(BM / UP, a.cout - co0);  // nco % 8 == 0 (launcher)
-        const int tl_n = BNP * UP;
-        const size_t pstride = (size_t)(a.cout >> 3) * a.ylen * 8;
-        for (int e = tid; e < (nco >> 3) * tl_n; e += NT) {
-          const int o = e / tl_n, tl = e - o * tl_n;
-          const int nl = tl / UP, ph = tl - nl * UP;
-          const int t = (p0 + nl) * UP + ph - a.up_pad;
-          if (p0 + nl >= a.ng || t < 0 || t >= a.ylen) continue;
-          float v[8], al[8], ia[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int co = co0 + 8 * o + u;
-            v[u] = ct[((8 * o + u) * UP + ph) * BNP + nl];
-            if (a.bias) v[u] = v[u] + a.bias[co];
-            if (a.y) a.y[((size_t)b * a.cout + co) * a.ylen + t] = v[u];
-            al[u] = a.alpha_o[co];
-            ia[u] = a.inv_alpha_o[co];
-          }
-          snake_n<8>(v, al, ia);
-          const size_t off =
-              ((((size_t)b * 3) * (a.cout >> 3) + ((co0 >> 3) + o)) * a.ylen + t) * 8;
-          store_planes8(a.ysp, pstride, off, v);
-        }
-      };
-      if (a.ysp) {
-        if (a.up == 8 && BM % 8 == 0) walk_planes(std::integral_constant<int, 8>{});
-        else if (a.up == 4 && BM % 4 == 0) walk_planes(std::integral_constant<int, 4>{});
-        else if (a.up == 2) walk_planes(std::integral_constant<int, 2>{});
-      } else if (a.up == 8 && BM % 8 == 0) walk4(std::integral_constant<int, 8>{});
+      if (a.up == 8 && BM % 8 == 0) walk4(std::integral_constant<int, 8>{});
       else if (a.up == 4 && BM % 4 == 0) walk4(std::integral_constant<int, 4>{});
       else if (a.up == 2) walk4(std::integral_constant<int, 2>{});
       else walk(std::integral_constant<int, 0>{});

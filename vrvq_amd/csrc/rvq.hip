@@ -49,8 +49,15 @@
     if ((buf) && threadIdx.x == 0)                                                         \
       (buf)[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
+// ... by thread t of the workgroup (the pt expansion's loader wave)
+#define FSTAMPT(buf, slot, t)                                                                \
+  do {                                                                                     \
+    if ((buf) && threadIdx.x == (t))                                                       \
+      (buf)[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
 #else
 #define FSTAMP(buf, slot) do {} while (0)
+#define FSTAMPT(buf, slot, t) do {} while (0)
 #endif
 
 namespace {
@@ -564,8 +571,10 @@ __global__ __launch_bounds__(PJ2_NT) void rvq_project3_kernel(const float* __res
 // One workgroup per CU: F = ceil(B*T / 256) frames each (<= 16).
 // Two barriers per stage; outputs stay in LDS until the epilogue.
 struct ChainArgs {
-  const float* part;   // [8][NF][nq*8]
+  const float* part;   // [8][NFS][nq*8]
   int B, T, nq, F, NF;
+  int NFS;             // split stride of part in frames (the three-launch path: NF; the fused
+                       // launch from the conv's partials: the frames of the whole call)
   const float* b_in;   // [nq][8]
   const float* qb;     // [nq][8]
   const float* mcol;   // [nq][nq][8][8]
@@ -663,8 +672,10 @@ struct ChainHandoff {              // fused launches only
 
 // Where a chain part gets pu = (P + b_in) - Qb of its frames: CH_SPLIT the 8 split partials of
 // the three-launch path (plain loads after the projection kernel), CH_GRANULE the tagged
-// partial granules of rvq_fused_kernel, CH_LOCAL already in LDS (rvq_fm_kernel's own projection).
-constexpr int CH_SPLIT = 0, CH_GRANULE = 1, CH_LOCAL = 2;
+// partial granules of rvq_fused_kernel, CH_LOCAL already in LDS (rvq_fm_kernel's own projection),
+// CH_PART the 8 split partials the encoder's last conv wrote in its epilogue (vrvq_conv1d_proj;
+// plain loads after that kernel's boundary) in rvq_pt_kernel, which publishes every stage.
+constexpr int CH_SPLIT = 0, CH_GRANULE = 1, CH_LOCAL = 2, CH_PART = 3;
 
 template <int NM, int MODE>
 __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0, int nf,
@@ -766,7 +777,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
       const int e = e0 + h * CH_NT;
       const size_t base = (size_t)n0 * R + (e < nf * R ? e : 0);
 #pragma unroll
-      for (int sp = 0; sp < PJ_SPLIT; ++sp) v[h][sp] = a.part[(size_t)sp * a.NF * R + base];
+      for (int sp = 0; sp < PJ_SPLIT; ++sp) v[h][sp] = a.part[(size_t)sp * a.NFS * R + base];
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1188,6 +1199,8 @@ struct FusedArgs {
                                     // bit 1 = chain parts skip the next stage's codebook
                                     // fragment loads (outputs wrong; timing only)
   int warm;                         // expansion workgroups pull the stage tables into L2 first
+  int xf;                           // rvq_pt_kernel expansion knobs (VRVQ_RVQ_XF, A/B): bit 0
+                                    // s_setprio(1) on the compute waves, bit 1 probe polls
 };
 
 // The stage tables the chain and the expansion read after stage 0 (normalised / raw codebooks,
@@ -1715,6 +1728,283 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fm_kernel(FusedArgs f) {
 }
 
 // ------------------------------------------------------------------------------------------
+// rvq_pt_kernel: the quantizer from the projection partials that the encoder's last conv wrote
+// in its epilogue (vrvq_conv1d_proj: part[8][B T][8 nq], rvq_project3_kernel's values bit for
+// bit). Neither z nor W_in is read here, and no projection sits in front of the chain.
+//   Workgroups [0, B P): chain parts (clip b, frames [p F, p F + F), F <= 16): the 8 partials
+// of their frames (plain loads: the conv kernel's boundary orders them) summed in split order
+// -- the three-launch chain's expression, so every output equals the three-launch path's bit
+// for bit -- then the chain, publishing every stage's zst as tagged granules.
+//   Workgroups after: expansion (clip b, 96-frame window fb, 128-channel block cb), 8 waves,
+// z_q_is and the masked z_q of the window's 4 x 3 (32-channel, 32-frame) tiles with
+// fused_expand_body's expressions (four v_mfma_f32_32x32x2_f32 per tile, DPP quad transpose,
+// 16-B stores of four frames of one channel), one channel tile ct = w & 3 per wave (waves w and
+// w + 4 share a SIMD: 3 tiles per SIMD): waves 0-2 frame tiles {0, 2}, wave 3 {0, 1}, waves 4-6
+// {1}, wave 7 {2}. Wave 7 is also the LOADER: per stage it polls the window's zst granules (6 x
+// 16 B per lane, tag-checked, bounded) into one half of a double-buffered LDS slab while every
+// wave runs the previous stage out of the other half; one barrier per stage. It issues the poll
+// BEFORE its own tile's stores and checks the tags after them: vmcnt retires in order, so the
+// check waits for the poll only, not for the stores. r05's expansion polled from every wave,
+// and where a look came too early its second look waited behind the wave's whole stage of stores
+// (a ~1 us bubble per stage while the chain was ahead). The loader also pulls the stage tables
+// into its XCD's L2 while it waits for stage 0 (off by default: VRVQ_RVQ_WARM=1).
+constexpr int PT_FB = 96;                          // frames per expansion window (3 tiles)
+constexpr int PT_LOADER = 7;                       // the loader wave
+constexpr int PT_SLAB = PT_FB * RCD;               // floats per slab half
+constexpr int PT_SL = PT_FB * 4 / 64;              // 16-B granule pairs per loader lane (6)
+constexpr int PT_NI = 2;                           // tiles per wave, at most
+constexpr int PT_ZQ = 2 * PT_SLAB + CH_NT;         // floats: the z_q accumulators
+constexpr int PT_NTILE = 12;                       // tiles of a window (4 x 3)
+constexpr int PT_EX_FLOATS = PT_ZQ + PT_NTILE * 16 * 64;  // slab, warm-up sink, accumulators
+
+struct PtOps {
+  float wa[4];    // W_out[c0 + col][k], k = h, 2 + h, 4 + h, 6 + h (the MFMA steps' A values)
+  float bb[4];    // b_out of the lane's four output channels (one per register quad)
+};
+
+// first accumulator slot of wave w (its tiles' slots are consecutive; 12 in all)
+__device__ __forceinline__ int pt_slot0(int w) { return w < 4 ? 2 * w : 4 + w; }
+// frame tile of slot j of wave w (-1: none)
+__device__ __forceinline__ int pt_tile(int w, int j) {
+  if (w < 3) return j == 0 ? 0 : 2;
+  if (w == 3) return j;
+  if (w < PT_LOADER) return j == 0 ? 1 : -1;
+  return j == 0 ? 2 : -1;
+}
+
+__device__ __forceinline__ void pt_expand_body(const FusedArgs& f, int e, int N, float* sm) {
+  const int nq = f.c.nq, T = f.c.T, F = f.c.F;
+  constexpr int NCB = RD / FU_CB;
+  const int cb = e % NCB;
+  const int fb = (e / NCB) % f.n_fb;
+  const int b = e / (NCB * f.n_fb);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wave == PT_LOADER;
+  const int col = lane & 31, h = lane >> 5;
+  const int nfr = min(PT_FB, T - fb * PT_FB);       // frames of this window (>= 1)
+  const int n_ft = (nfr + 31) / 32;
+  // the slab window: PT_FB frames from wlo (the last window ends at the clip's last frame, so it
+  // holds the moved-back last tile). Partial last tiles instead (no frame written twice; 9 of
+  // every 96 frames' z_q_is rows are at T = 87) measured slower: 41.75 vs 39.2-40.6 us per
+  // launch, each stage's stores 0.3-0.8 us longer (profiles/r06f_stamps.log)
+  const int wlo = T >= PT_FB ? min(fb * PT_FB, T - PT_FB) : 0;
+  const __amdgpu_buffer_rsrc_t zr =
+      __builtin_amdgcn_make_buffer_rsrc(f.zsh, (short)0, f.zsh_bytes, RSRC_FLAGS);
+  const int zstage = f.P * FU_ROWS * RCD * 8;  // bytes per stage
+  const unsigned base = f.epoch * 64u;
+  __shared__ int xdead_s;  // the loader's wait ran out (then no wait any more; outputs NaN)
+  if (tid == 0) xdead_s = 0;
+
+  // ---- loader: lane item q = lane + 64 u -> frame wlo + (q >> 2), slots 2 (q & 3) + {0, 1}
+  // (frames past the clip re-read its last one: loaded, never used)
+  auto soff = [&](int u) {
+    const int q = lane + 64 * u;
+    const int t = min(wlo + (q >> 2), T - 1);
+    const int p = t / F, fr = t - p * F;
+    return ((((b * nq) * f.P + p) * FU_ROWS + fr) * RCD + 2 * (q & 3)) * 8;
+  };
+  // ---- compute state: the wave's channel tile and its frame tiles (wave-uniform activity)
+  const int c0 = cb * FU_CB + (wave & 3) * 32;
+  const int crow = c0 + col;                  // A-operand row (W_out) of this lane
+  const int chk = c0 + 4 * h + (lane & 3);    // after the transpose: channels chk + 8 qd
+  const size_t wstride = (size_t)RD * RCD;
+  int tbs[PT_NI];  // the tiles' first frames (wave-uniform)
+  unsigned nact[PT_NI];
+  bool act[PT_NI];
+#pragma unroll
+  for (int j = 0; j < PT_NI; ++j) {
+    const int ft = pt_tile(wave, j);
+    act[j] = ft >= 0 && ft < n_ft;
+    // the tile's first frame; a clip's last, partial tile is moved back to end at the clip's last
+    // frame (it overlaps the tile before it: those frames are written twice, identical values)
+    int tb = fb * PT_FB + max(ft, 0) * 32;
+    if (tb + 32 > T && T >= 32) tb = T - 32;
+    tbs[j] = __builtin_amdgcn_readfirstlane(tb);
+    float sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = min(max(tb + 4 * (col >> 2) + u, 0), T - 1);
+      sv[u] = f.c.imp ? (f.c.imp[(size_t)b * T + t] * f.c.level) * (float)nq : INFINITY;
+    }
+    unsigned w = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // mask[b,i,t] = (s - i >= 0), s = (imp * level) * nq (models/utils.py:45-61): the first
+      // floor(s) + 1 stages (none for NaN or s < 0, all nq for s >= nq - 1 or CBR's inf)
+      const int n = sv[u] >= 0.0f ? (int)floorf(fminf(sv[u], (float)(nq - 1))) + 1 : 0;
+      w |= (unsigned)n << (8 * u);
+    }
+    nact[j] = w;
+  }
+  // the lane's B-operand frame (col) as a slab row, and the first of its four output frames
+  auto trow = [&](int j) { return min(max(tbs[j] - wlo + col, 0), PT_FB - 1); };
+  auto tq = [&](int j) { return tbs[j] + 4 * (col >> 2); };
+  auto load_ops = [&](int i, PtOps& o) {
+    const float* wp = f.w_out + (size_t)i * wstride + (size_t)crow * RCD + h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) o.wa[s] = wp[2 * s];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) o.bb[qd] = f.b_out[(size_t)i * RD + chk + 8 * qd];
+  };
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  auto store_quad = [&](float* row, int t, float v0, float v1, float v2, float v3) {
+    if (t + 4 <= T) {
+      *reinterpret_cast<f4u*>(row + t) = f4u{v0, v1, v2, v3};
+    } else if (t < T) {  // a clip shorter than a frame tile
+      row[t] = v0;
+      if (t + 1 < T) row[t + 1] = v1;
+      if (t + 2 < T) row[t + 2] = v2;
+    }
+  };
+  // the masked z_q accumulators live in LDS ([slot][quad][lane] float4: conflict-free 16-B
+  // accesses; in registers they spilled at the 128-VGPR budget with three tiles per wave, and a
+  // spill reload would wait behind the stage's stores)
+  float4* zacc = reinterpret_cast<float4*>(sm + PT_ZQ) + pt_slot0(wave) * (4 * 64) + lane;
+#pragma unroll
+  for (int j = 0; j < PT_NI; ++j)
+    if (pt_tile(wave, j) >= 0)
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) zacc[(j * 4 + qd) * 64] = make_float4(0.f, 0.f, 0.f, 0.f);
+  PtOps cur;
+  load_ops(0, cur);
+  // idle until stage 0 lands (~6 us): the loader may pull the stage tables into this XCD's L2
+  // (fm kernel, r05) before its first poll
+  if (loader && f.warm) warm_tables(f, e, (int)gridDim.x - f.c.B * f.P, N, sm + 2 * PT_SLAB);
+  __syncthreads();  // xdead_s initialised
+  bool dead = false;
+  u32x4 g[PT_SL];
+  // iteration i: the loader fills slab half (i & 1) with stage i while every wave runs stage
+  // i - 1 from the other half
+  for (int i = 0; i <= nq; ++i) {
+    const bool poll = loader && i < nq && !dead;
+    const unsigned tag = base + (unsigned)i + 1u;
+    if (poll)  // issued ahead of this wave's stores below
+#pragma unroll
+      for (int u = 0; u < PT_SL; ++u)
+        g[u] = __builtin_amdgcn_raw_buffer_load_b128(zr, soff(u) + i * zstage, 0, CPOL_SC1);
+    if (i > 0) {
+      const int si = i - 1;  // the stage computed now
+      FSTAMP(f.stamps, 1 + si);
+      // the next stage's operands ahead of this stage's stores (vmcnt retires in order)
+      PtOps nxt;
+      load_ops(min(si + 1, nq - 1), nxt);
+      const float* slab = sm + (si & 1) * PT_SLAB;
+#pragma unroll
+      for (int j = 0; j < PT_NI; ++j) {
+        if (!act[j]) continue;
+        const float4 zb = *reinterpret_cast<const float4*>(slab + trow(j) * RCD + 4 * h);
+        f32x16 q;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) q[r] = 0.0f;
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.wa[0], zb.x, q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.wa[1], zb.y, q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.wa[2], zb.z, q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.wa[3], zb.w, q, 0, 0, 0);
+        quad_transpose(q, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) q[r] = q[r] + cur.bb[r >> 2];
+        if (dead)  // wave-uniform (a timed-out wait): poisoned outputs
+#pragma unroll
+          for (int r = 0; r < 16; ++r) q[r] = __builtin_nanf("");
+        if (f.z_q_is) {
+#pragma unroll
+          for (int qd = 0; qd < 4; ++qd) {
+            float* row = f.z_q_is + (((size_t)b * nq + si) * RD + chk + 8 * qd) * T;
+            store_quad(row, tq(j), q[4 * qd], q[4 * qd + 1], q[4 * qd + 2], q[4 * qd + 3]);
+          }
+        }
+        float m[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned n = (nact[j] >> (8 * u)) & 0xffu;
+          m[u] = (unsigned)si < n ? 1.0f : 0.0f;  // models/utils.py:45-61
+        }
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          float4 a = zacc[(j * 4 + qd) * 64];
+          a.x = a.x + q[4 * qd] * m[0];
+          a.y = a.y + q[4 * qd + 1] * m[1];
+          a.z = a.z + q[4 * qd + 2] * m[2];
+          a.w = a.w + q[4 * qd + 3] * m[3];
+          zacc[(j * 4 + qd) * 64] = a;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one tile's 16 values live at a time
+      }
+      if (si < 8) FSTAMP(f.stamps, 48 + si);  // the stage's stores issued (thread 0)
+      cur = nxt;
+    }
+    if (poll) {
+      for (unsigned it = 0;; ++it) {
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u) ok = ok && g[u][1] == tag && g[u][3] == tag;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (it >= f.spin_max) {
+          if (lane == 0) {
+            report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
+            xdead_s = 1;
+          }
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u)
+          g[u] = __builtin_amdgcn_raw_buffer_load_b128(zr, soff(u) + i * zstage, 0, CPOL_SC1);
+      }
+      if (i < 8) FSTAMPT(f.stamps, 56 + i, 64 * PT_LOADER);  // the stage's rows seen
+      float* slab = sm + (i & 1) * PT_SLAB;
+#pragma unroll
+      for (int u = 0; u < PT_SL; ++u) {
+        const int q = lane + 64 * u;
+        *reinterpret_cast<float2*>(slab + (q >> 2) * RCD + 2 * (q & 3)) =
+            make_float2(__uint_as_float(g[u][0]), __uint_as_float(g[u][2]));
+      }
+    }
+    __syncthreads();  // slab half (i & 1) holds stage i; half ((i - 1) & 1) is free
+    dead = xdead_s != 0;
+  }
+  FSTAMP(f.stamps, 40);
+#pragma unroll
+  for (int j = 0; j < PT_NI; ++j) {
+    if (!act[j]) continue;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      float* row = f.z_q + ((size_t)b * RD + chk + 8 * qd) * T;
+      const float d = dead ? __builtin_nanf("") : 0.0f;
+      const float4 a = zacc[(j * 4 + qd) * 64];
+      store_quad(row, tq(j), a.x + d, a.y + d, a.z + d, a.w + d);
+    }
+  }
+}
+
+template <int NM>
+__global__ __launch_bounds__(CH_NT, 4) void rvq_pt_kernel(FusedArgs f) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = f.c.B, T = f.c.T, F = f.c.F;
+  int blk = blockIdx.x;
+  FSTAMP(f.stamps, 0);
+  if ((f.xf & 4) && gridDim.x == 512 && B * f.P == 256) {
+    // A/B (VRVQ_RVQ_XF bit 2): roles by the observed dispatch order (block b -> XCD b % 8, that
+    // XCD's CU (b / 8) % 32, slot b / 256; speed only, any placement is correct): chain parts on
+    // CUs 0-15 of every XCD (two per CU), expansion on CUs 16-31
+    const int sl = blk >> 8, cu = (blk >> 3) & 31, x = blk & 7;
+    blk = cu < 16 ? sl * 128 + cu * 8 + x : 256 + sl * 128 + (cu - 16) * 8 + x;
+  }
+  if (blk >= B * f.P) {
+    pt_expand_body(f, blk - B * f.P, 256 * NM, sm);
+    FSTAMP(f.stamps, 41);
+    return;
+  }
+  const int b = blk / f.P, p = blk - b * f.P;
+  const int t0 = p * F, nf = min(F, T - t0);
+  if (f.stall && blk == 0)  // test knob (vrvq_rvq_debug_stall): a late producer
+    for (unsigned k = 0; k < f.stall; ++k) __builtin_amdgcn_s_sleep(127);
+  chain_body<NM, CH_PART>(f.c, sm, b * T + t0, nf, fused_handoff(f, b, p));
+}
+
+// ------------------------------------------------------------------------------------------
 // Projection kernel: 2 = rvq_project2_kernel (one workgroup per clip x split, default), 1 =
 // rvq_project_kernel (48-frame tiles x 64-row blocks). Same partials bit for bit (A/B timing and
 // the bit-identity test; VRVQ_RVQ_PROJECT=1 in the environment).
@@ -1790,6 +2080,7 @@ int launch_chain(const ChainArgs& a0, int ncode, hipStream_t st) {
   F = F < 1 ? 1 : (F > CH_FMAX ? CH_FMAX : F);
   a.F = (int)F;
   a.NF = (int)nf;
+  a.NFS = a.NFS ? a.NFS : (int)nf;
   const long long nblk = (nf + F - 1) / F;
   VRVQ_CHECK_ARG(nblk < 0x7fffffffLL);
   switch (ncode / 256) {
@@ -1867,6 +2158,7 @@ unsigned g_epoch = 1;                 // last epoch handed out (guarded by g_fu_
 unsigned* g_err_host = nullptr;       // host-mapped error word
 unsigned* g_err_host_dev = nullptr;   // its device address
 unsigned g_spin_max = SPIN_MAX;       // vrvq_rvq_debug (timeout test)
+int g_pt_cap_limit = 0x7fffffff;      // vrvq_rvq_debug_capacity (fallback test)
 unsigned g_stall = 0;
 constexpr unsigned EPOCH_RESET = 1u << 24;  // 64 epoch + stage stays below 2^32
 
@@ -2120,6 +2412,96 @@ int launch_fm_nm(const FusedArgs& f0, int batch, int frames, int nq, const float
     f.P = P;
     f.n_fb = n_fb;
     const int rc = launch_timed(rvq_fm_kernel<NM>, (unsigned)(bc * wpc), lds, st, f);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// Frames per chain part of rvq_pt_kernel: as rvq_fm_kernel (8 parts up to T = 128, else 16
+// frames), fewer wherever the chain's LDS would not fit twice per CU.
+size_t pt_lds_bytes(int nq, int F, int N) {
+  size_t c = (size_t)ChainLds(nq, F, N).total * sizeof(float);
+  const size_t ex = (size_t)PT_EX_FLOATS * sizeof(float);  // slab, warm-up sink, one z_q tile
+  return c < ex ? ex : c;
+}
+int pt_frames_per_part(int frames, int nq, int N) {
+  static const int f_env = [] {  // VRVQ_RVQ_PT_F: frames per chain part (A/B; 1..16)
+    const char* e = getenv("VRVQ_RVQ_PT_F");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= FU_ROWS ? v : 0;
+  }();
+  // 16 frames per part: fewer, longer chain parts measured fastest at T = 87 (in-step 43.1-43.5
+  // us vs 44.2 at F = 11, 44.4-44.8 at 12; profiles/r06g_ab.txt)
+  const int F0 = f_env ? min(f_env, frames) : min(FU_ROWS, frames);
+  for (int F = F0; F >= 1; --F)
+    if (pt_lds_bytes(nq, F, N) <= 80 * 1024) return F;
+  return 0;
+}
+size_t pt_zst_bytes(int batch, int frames, int nq) { return (size_t)batch * nq * frames * RCD * 4; }
+
+// Clips per rvq_pt_kernel launch (every workgroup resident), 0 when not even one clip fits or the
+// three launches are selected (vrvq_rvq_path(1)).
+template <int NM>
+int pt_capacity(int frames, int nq, int* F_out, int* P_out, int* n_fb_out, size_t* lds_out) {
+  const int F = pt_frames_per_part(frames, nq, 256 * NM);
+  if (F < 1 || rvq_path() == 1) return 0;
+  const int P = (frames + F - 1) / F;
+  const int n_fb = (frames + PT_FB - 1) / PT_FB;
+  const size_t lds = pt_lds_bytes(nq, F, 256 * NM);
+  const int wpc = P + (RD / FU_CB) * n_fb;
+  *F_out = F;
+  *P_out = P;
+  *n_fb_out = n_fb;
+  *lds_out = lds;
+  return min(fused_clip_capacity((const void*)rvq_pt_kernel<NM>, lds, wpc), g_pt_cap_limit);
+}
+
+// The quantizer from the conv's partials: rvq_pt_kernel per group of resident clips, or -- the
+// shape does not fit (a clip longer than the resident grid) or vrvq_rvq_path(1) -- the chain and
+// the expansion as two stream-ordered launches over the same partials (zst through the
+// workspace). Both give the same outputs bit for bit.
+template <int NM>
+int launch_pt_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* part,
+                 const float* imp, int64_t* codes, float* latents, float* loss_pf, float* z_q_is,
+                 float* z_q, float* mask, void* ws, size_t ws_bytes, hipStream_t st) {
+  int F = 0, P = 0, n_fb = 0;
+  size_t lds = 0;
+  const int cap = pt_capacity<NM>(frames, nq, &F, &P, &n_fb, &lds);
+  const int R = nq * RCD;
+  if (cap < 1) {
+    if (ws_bytes < pt_zst_bytes(batch, frames, nq)) return VRVQ_ERR_ARG;
+    float* zst = static_cast<float*>(ws);
+    ChainArgs a = f0.c;
+    a.part = part; a.B = batch; a.T = frames; a.nq = nq; a.NFS = 0;
+    a.imp = imp; a.codes = codes; a.latents = latents; a.loss_pf = loss_pf; a.zst = zst;
+    a.mask = mask;
+    int rc = launch_chain(a, 256 * NM, st);
+    if (rc) return rc;
+    return launch_expand(zst, batch, RD, frames, nq, f0.w_out, f0.b_out, imp, f0.c.level, z_q_is,
+                         z_q, nullptr, st);
+  }
+  int bc_max = min(batch, cap);
+  while (bc_max > 1 && zsh_bytes(bc_max, nq, P) > 0x7fffffffULL) --bc_max;
+  const size_t need = zsh_bytes(bc_max, nq, P);
+  const int wpc = P + (RD / FU_CB) * n_fb;
+  for (int b0 = 0; b0 < batch; b0 += bc_max) {
+    const int bc = min(bc_max, batch - b0);
+    FusedArgs f = f0;
+    FusedLaunch L;
+    if (!fused_prepare(st, need, ws, ws_bytes, &L)) return VRVQ_ERR_UNSUPPORTED;
+    fused_chunk_args(f, b0, bc, frames, nq, F, nullptr, imp, codes, latents, loss_pf, z_q_is, z_q,
+                     mask);
+    f.z = nullptr;
+    f.z_q = z_q + (size_t)b0 * RD * frames;
+    f.c.part = part + (size_t)b0 * frames * R;  // the chunk's frames within every split
+    f.c.NFS = batch * frames;                   // split stride: the call's frames
+    f.sync = L.sync;
+    f.epoch = L.epoch;
+    f.zsh = reinterpret_cast<unsigned long long*>(L.area);
+    f.zsh_bytes = (int)zsh_bytes(bc, nq, P);
+    f.P = P;
+    f.n_fb = n_fb;
+    const int rc = launch_timed(rvq_pt_kernel<NM>, (unsigned)(bc * wpc), lds, st, f);
     if (rc) return rc;
   }
   return 0;
@@ -2440,4 +2822,85 @@ extern "C" int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frame
     case 3: return launch_fm_nm<3>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
     default: return launch_fm_nm<4>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
   }
+}
+
+extern "C" int vrvq_rvq_workspace_part(int batch, int frames, int nq, int ncode, long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0 && ncode > 0);
+  if (nq > CH_NQMAX || ncode % 256 != 0 || ncode > 1024) return VRVQ_ERR_UNSUPPORTED;
+  // the fused launch's granules under stream capture (+ its sync block), or the two-launch
+  // fallback's zst rows: the larger
+  long long g = 0;
+  const int F = pt_frames_per_part(frames, nq, ncode);
+  if (F >= 1) g = (long long)zsh_bytes(batch, nq, (frames + F - 1) / F) + (long long)FU_SYNC_BYTES;
+  const long long z = (long long)pt_zst_bytes(batch, frames, nq);
+  *bytes = g > z ? g : z;
+  return 0;
+}
+
+extern "C" int vrvq_rvq_encode_part(const float* part, int batch, int dim, int frames, int nq,
+                                    int ncode, int cdim, const float* b_in, const float* cb,
+                                    const float* cbf, const float* c2, const float* w_out,
+                                    const float* b_out, const float* mcol, const float* qb,
+                                    const float* imp, float level, int64_t* codes,
+                                    float* latents, float* loss_pf, float* z_q_is, float* z_q,
+                                    float* mask, void* workspace, long long workspace_bytes,
+                                    vrvq_stream_t stream) {
+  VRVQ_CHECK_ARG(part && b_in && cb && cbf && c2 && w_out && b_out && mcol && qb && codes &&
+                 latents && loss_pf && z_q && workspace);
+  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0);
+  VRVQ_CHECK_ARG(((uintptr_t)workspace & 15) == 0 && ((uintptr_t)part & 15) == 0);
+  if (!rvq_shape_ok(dim, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  VRVQ_CHECK_ARG((long long)batch * frames * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
+  long long need = 0;
+  const int rc0 = vrvq_rvq_workspace_part(batch, frames, nq, ncode, &need);
+  if (rc0) return rc0;
+  VRVQ_CHECK_ARG(workspace_bytes >= need);
+  FusedArgs f{};
+  ChainArgs& c = f.c;
+  c.b_in = b_in; c.qb = qb; c.mcol = mcol; c.cb = cb; c.cbf = cbf; c.c2 = c2;
+  c.level = level;
+  f.w_out = w_out;
+  f.b_out = b_out;
+  // VRVQ_RVQ_WARM=1: the loader warms the stage tables' L2 first (A/B; measured slower here:
+  // stage 0 lands at ~6 us, profiles/r06f_ab.txt, r06c_ab.txt)
+  static const int warm = [] {
+    const char* e = getenv("VRVQ_RVQ_WARM");
+    return e ? atoi(e) : 0;
+  }();
+  f.warm = warm;
+  static const int xf = [] {  // VRVQ_RVQ_XF: the expansion's A/B knobs (FusedArgs::xf)
+    const char* e = getenv("VRVQ_RVQ_XF");
+    return e ? atoi(e) : 0;
+  }();
+  f.xf = xf;
+  hipStream_t st = as_stream(stream);
+  const size_t wsb = (size_t)workspace_bytes;
+  switch (ncode / 256) {
+    case 1: return launch_pt_nm<1>(f, batch, frames, nq, part, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    case 2: return launch_pt_nm<2>(f, batch, frames, nq, part, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    case 3: return launch_pt_nm<3>(f, batch, frames, nq, part, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+    default: return launch_pt_nm<4>(f, batch, frames, nq, part, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
+  }
+}
+
+extern "C" int vrvq_rvq_fused_clips(int frames, int nq, int ncode, int* clips) {
+  VRVQ_CHECK_ARG(clips && frames > 0 && nq > 0);
+  *clips = 0;
+  if (!rvq_shape_ok(RD, RCD, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
+  int F = 0, P = 0, n_fb = 0;
+  size_t lds = 0;
+  switch (ncode / 256) {
+    case 1: *clips = pt_capacity<1>(frames, nq, &F, &P, &n_fb, &lds); break;
+    case 2: *clips = pt_capacity<2>(frames, nq, &F, &P, &n_fb, &lds); break;
+    case 3: *clips = pt_capacity<3>(frames, nq, &F, &P, &n_fb, &lds); break;
+    default: *clips = pt_capacity<4>(frames, nq, &F, &P, &n_fb, &lds); break;
+  }
+  if (*clips < 0) *clips = 0;
+  return 0;
+}
+
+extern "C" int vrvq_rvq_debug_capacity(int clips) {
+  const int prev = g_pt_cap_limit;
+  g_pt_cap_limit = clips >= 0 ? clips : 0x7fffffff;
+  return prev;
 }

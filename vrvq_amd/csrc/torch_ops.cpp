@@ -164,7 +164,7 @@ const uint16_t* x3_ptr(const optional<Tensor>& w3, const Tensor& ref, int64_t ci
 std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef shape,
                                             const optional<Tensor>& alpha_out,
                                             const optional<Tensor>& inv_alpha_out,
-                                            bool want_raw, bool no_ys = false) {
+                                            bool want_raw) {
   TORCH_CHECK(alpha_out.has_value() == inv_alpha_out.has_value(),
               "out_snake: alpha_out and inv_alpha_out go together");
   if (alpha_out.has_value()) {
@@ -173,7 +173,7 @@ std::tuple<Tensor, Tensor, Tensor> out_pair(const Tensor& like, at::IntArrayRef 
     TORCH_CHECK(alpha_out->numel() == shape[1] && inv_alpha_out->numel() == shape[1],
                 "out_snake: one alpha per output channel");
   }
-  Tensor ys = (alpha_out.has_value() && !no_ys) ? empty_f(shape, like) : none_like(like);
+  Tensor ys = alpha_out.has_value() ? empty_f(shape, like) : none_like(like);
   Tensor y = (want_raw || !alpha_out.has_value()) ? empty_f(shape, like) : none_like(like);
   return {y, ys, Tensor()};
 }
@@ -182,12 +182,6 @@ float* opt_ptr(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 
 // Snake1d -> WNConv1d (+ residual, Tanh / Sigmoid, next Snake), models/layers.py:17-41, 52-89;
 // models/dac_vrvq.py:27-34, 62-74; models/importance_subnet.py:38-45.
-// snake(x) as three bf16 planes (B, 3, C / 8, T, 8) int16 (include/vrvq.h vrvq_conv1d_ex)
-Tensor planes_like(const Tensor& like, int64_t B, int64_t C, int64_t T) {
-  TORCH_CHECK(C % 8 == 0, "planes: channels must be a multiple of 8");
-  return at::empty({B, 3, C / 8, T, 8}, like.options().dtype(at::kShort));
-}
-
 std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed, int64_t cout,
                                         int64_t stride, int64_t pad, int64_t dil,
                                         const optional<Tensor>& bias,
@@ -196,24 +190,18 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
                                         const optional<Tensor>& residual, int64_t epilogue,
                                         const optional<Tensor>& alpha_out,
                                         const optional<Tensor>& inv_alpha_out, bool want_raw,
-                                        const optional<Tensor>& w_x3, bool ys_planes) {
-  // x: (B, C, T) fp32, or snake(x) as planes (B, 3, C / 8, T, 8) int16 (the k7 planes tile)
-  const bool x_planes = x.scalar_type() == at::kShort;
-  check_t(x, "x", x_planes ? at::kShort : at::kFloat);
+                                        const optional<Tensor>& w_x3) {
+  check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
   check_opt(alpha, x, "alpha");
   check_opt(inv_alpha, x, "inv_alpha");
   check_opt(residual, x, "residual");
-  TORCH_CHECK(x_planes ? (x.dim() == 5 && x.size(1) == 3 && x.size(4) == 8) : x.dim() == 3,
-              "conv1d: x must be (B, C, T) fp32 or planes (B, 3, C/8, T, 8) int16");
-  const int64_t B = x.size(0);
-  const int64_t cin = x_planes ? x.size(2) * 8 : x.size(1);
-  const int64_t tin = x_planes ? x.size(3) : x.size(2);
+  TORCH_CHECK(x.dim() == 3, "conv1d: x must be (B, C, T)");
+  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
   TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == cin,
               "conv1d: w_packed must be (Cin, k, cout_pad) with Cin = x's channels");
   TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(), "conv1d: snake needs inv_alpha");
-  TORCH_CHECK(!ys_planes || alpha_out.has_value(), "conv1d: planes output needs out_snake");
   c10::DeviceGuard guard(x.device());
   const int64_t k = w_packed.size(1), cout_pad = w_packed.size(2);
   const int64_t tout = (tin + 2 * pad - dil * (k - 1) - 1) / stride + 1;
@@ -221,20 +209,17 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
   if (residual.has_value())
     TORCH_CHECK(residual->sizes() == at::IntArrayRef({B, cout, tout}),
                 "conv1d: residual shape must equal the output shape");
-  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw, ys_planes);
-  if (ys_planes) ys = planes_like(x, B, cout, tout);
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
   // strided conv (k = 2 stride): w_x3 holds the planes of the phase-split weight (Cin * stride
   // view channels, 2 taps; include/vrvq.h vrvq_conv1d)
   const uint16_t* w3 = stride > 1 ? x3_ptr(w_x3, x, cin * stride, 2, cout_pad)
                                   : x3_ptr(w_x3, x, cin, k, cout_pad);
-  check_rc(vrvq_conv1d_ex(x.data_ptr(), x_planes ? 1 : 0, (int)B, (int)cin, (int)tin, fp(alpha),
-                          fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad,
-                          (int)k, (int)stride, (int)pad, (int)dil, fp(bias), fp(residual),
-                          (int)epilogue, y.numel() ? y.data_ptr<float>() : nullptr, (int)tout,
-                          fp(alpha_out), fp(inv_alpha_out), ys_planes ? nullptr : opt_ptr(ys),
-                          ys_planes ? reinterpret_cast<uint16_t*>(ys.data_ptr<int16_t>()) : nullptr,
-                          stream_of(x)),
-           "vrvq_conv1d_ex");
+  check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                       fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad,
+                       (int)k, (int)stride, (int)pad, (int)dil, fp(bias), fp(residual),
+                       (int)epilogue, y.numel() ? y.data_ptr<float>() : nullptr, (int)tout,
+                       fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
+           "vrvq_conv1d");
   return {y, ys};
 }
 
@@ -273,7 +258,7 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
     const optional<Tensor>& bias, const optional<Tensor>& alpha,
     const optional<Tensor>& inv_alpha, const optional<Tensor>& alpha_out,
     const optional<Tensor>& inv_alpha_out, bool want_raw, int64_t pad,
-    const optional<Tensor>& w_x3, bool ys_planes) {
+    const optional<Tensor>& w_x3) {
   check_t(x, "x");
   check_on(w_packed, x, "w_packed");
   check_opt(bias, x, "bias");
@@ -290,19 +275,14 @@ std::tuple<Tensor, Tensor> snake_conv_transpose1d(
   c10::DeviceGuard guard(x.device());
   const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
   const int64_t tout = (tin - 1) * stride - 2 * p + 2 * stride;
-  TORCH_CHECK(!ys_planes || alpha_out.has_value(), "conv_transpose1d: planes output needs out_snake");
-  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw, ys_planes);
-  if (ys_planes) ys = planes_like(x, B, cout, tout);
+  auto [y, ys, _u] = out_pair(x, {B, cout, tout}, alpha_out, inv_alpha_out, want_raw);
   const uint16_t* w3 = x3_ptr(w_x3, x, cin, 2, w_packed.size(2));
-  check_rc(vrvq_conv_transpose1d_ex(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                                    fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
-                                    (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
-                                    opt_ptr(y), fp(alpha_out), fp(inv_alpha_out),
-                                    ys_planes ? nullptr : opt_ptr(ys),
-                                    ys_planes ? reinterpret_cast<uint16_t*>(ys.data_ptr<int16_t>())
-                                              : nullptr,
-                                    stream_of(x)),
-           "vrvq_conv_transpose1d_ex");
+  check_rc(vrvq_conv_transpose1d_pad(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                                     fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
+                                     (int)w_packed.size(2), (int)stride, (int)p, fp(bias),
+                                     opt_ptr(y), fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
+                                     stream_of(x)),
+           "vrvq_conv_transpose1d_pad");
   return {y, ys};
 }
 
@@ -526,6 +506,103 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode_fm(
                               opt_ptr(mask), ws.numel() ? ws.data_ptr<float>() : nullptr,
                               (long long)ws.numel() * 4, stream_of(zt)),
            "vrvq_rvq_encode_fm");
+  return {codes, latents, loss_pf, z_q_is, z_q, mask};
+}
+
+// Snake1d -> WNConv1d (the encoder's last conv, models/dac_vrvq.py:33-34) with the in_proj of
+// every RVQ stage in its epilogue (include/vrvq.h vrvq_conv1d_proj): returns the partials
+// part (8, B*T, 8 nq) and, when want_z, z (B, 1024, T) as well (else an empty tensor).
+std::tuple<Tensor, Tensor> snake_conv1d_proj(const Tensor& x, const Tensor& w_packed,
+                                             int64_t cout, int64_t pad, int64_t dil,
+                                             const optional<Tensor>& bias,
+                                             const optional<Tensor>& alpha,
+                                             const optional<Tensor>& inv_alpha,
+                                             const optional<Tensor>& w_x3, const Tensor& w3in,
+                                             int64_t nq, bool want_z) {
+  check_t(x, "x");
+  check_on(w_packed, x, "w_packed");
+  check_opt(bias, x, "bias");
+  check_opt(alpha, x, "alpha");
+  check_opt(inv_alpha, x, "inv_alpha");
+  check_on(w3in, x, "w3in", at::kShort);
+  TORCH_CHECK(x.dim() == 3, "conv1d_proj: x must be (B, C, T)");
+  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1),
+              "conv1d_proj: w_packed must be (Cin, k, cout_pad) with Cin = x.shape[1]");
+  TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(), "conv1d_proj: snake needs inv_alpha");
+  c10::DeviceGuard guard(x.device());
+  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
+  const int64_t k = w_packed.size(1), cout_pad = w_packed.size(2);
+  const int64_t tout = tin + 2 * pad - dil * (k - 1);
+  TORCH_CHECK(tout > 0, "conv1d_proj: input too short");
+  long long n3 = 0;
+  check_rc(vrvq_rvq_w_in_planes_size((int)nq, (int)cout, 8, &n3), "vrvq_rvq_w_in_planes_size");
+  TORCH_CHECK(w3in.numel() == n3, "conv1d_proj: w3in must be rvq_pack_w_in(w_in_t) of nq stages");
+  Tensor part = empty_f({8, B * tout, nq * 8}, x);
+  Tensor z = want_z ? empty_f({B, cout, tout}, x) : none_like(x);
+  check_rc(vrvq_conv1d_proj(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                            fp(inv_alpha), w_packed.data_ptr<float>(),
+                            x3_ptr(w_x3, x, cin, k, cout_pad), (int)cout, (int)cout_pad, (int)k,
+                            (int)pad, (int)dil, fp(bias), opt_ptr(z), (int)tout,
+                            reinterpret_cast<const uint16_t*>(w3in.data_ptr<int16_t>()), (int)nq,
+                            part.data_ptr<float>(), stream_of(x)),
+           "vrvq_conv1d_proj");
+  return {part, z};
+}
+
+// The quantizer from vrvq_conv1d_proj's partials (include/vrvq.h vrvq_rvq_encode_part): the
+// six outputs of rvq_encode, equal to its three launches bit for bit.
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode_part(
+    const Tensor& part, int64_t frames, const Tensor& b_in, const Tensor& cb, const Tensor& cbf,
+    const Tensor& c2, const Tensor& w_out, const Tensor& b_out, const Tensor& mcol,
+    const Tensor& qb, const optional<Tensor>& imp, double level, bool want_z_q_is,
+    bool want_mask) {
+  check_pending_rvq_error();
+  check_t(part, "part");
+  check_on(b_in, part, "b_in");
+  check_on(cb, part, "cb");
+  check_on(cbf, part, "cbf");
+  check_on(c2, part, "c2");
+  check_on(w_out, part, "w_out");
+  check_on(b_out, part, "b_out");
+  check_on(mcol, part, "mcol");
+  check_on(qb, part, "qb");
+  check_opt(imp, part, "imp");
+  c10::DeviceGuard guard(part.device());
+  TORCH_CHECK(cb.dim() == 3, "rvq_encode_part: cb must be (nq, N, d)");
+  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2), T = frames;
+  TORCH_CHECK(T > 0 && part.dim() == 3 && part.size(0) == 8 && part.size(2) == nq * d &&
+                  part.size(1) % T == 0,
+              "rvq_encode_part: part must be (8, B*T, nq*d) from conv1d_proj");
+  const int64_t B = part.size(1) / T;
+  TORCH_CHECK(w_out.dim() == 3 && w_out.size(0) == nq && w_out.size(2) == d,
+              "rvq_encode_part: w_out must be (nq, D, d)");
+  const int64_t D = w_out.size(1);
+  TORCH_CHECK(b_out.numel() == nq * D && b_in.numel() == nq * d && c2.numel() == nq * N &&
+                  cbf.numel() == cb.numel(),
+              "rvq_encode_part: stage weights do not match cb");
+  TORCH_CHECK(mcol.numel() == nq * nq * d * d && qb.numel() == nq * d,
+              "rvq_encode_part: cross terms (rvq_cross_prep) do not match nq");
+  if (imp.has_value()) TORCH_CHECK(imp->numel() == B * T, "rvq_encode_part: imp must hold B*T values");
+  Tensor codes = at::empty({B, nq, T}, part.options().dtype(at::kLong));
+  Tensor latents = empty_f({B, nq * d, T}, part);
+  Tensor loss_pf = empty_f({B, nq, T}, part);
+  Tensor z_q_is = want_z_q_is ? empty_f({B, nq, D, T}, part) : none_like(part);
+  Tensor z_q = empty_f({B, D, T}, part);
+  Tensor mask = want_mask ? empty_f({B, nq, T}, part) : none_like(part);
+  long long ws_bytes = 0;
+  check_rc(vrvq_rvq_workspace_part((int)B, (int)T, (int)nq, (int)N, &ws_bytes),
+           "vrvq_rvq_workspace_part");
+  Tensor ws = at::empty({(ws_bytes + 3) / 4}, part.options().dtype(at::kFloat));
+  check_rc(vrvq_rvq_encode_part(part.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)N,
+                                (int)d, b_in.data_ptr<float>(), cb.data_ptr<float>(),
+                                cbf.data_ptr<float>(), c2.data_ptr<float>(),
+                                w_out.data_ptr<float>(), b_out.data_ptr<float>(),
+                                mcol.data_ptr<float>(), qb.data_ptr<float>(), fp(imp),
+                                (float)level, codes.data_ptr<int64_t>(),
+                                latents.data_ptr<float>(), loss_pf.data_ptr<float>(),
+                                opt_ptr(z_q_is), z_q.data_ptr<float>(), opt_ptr(mask),
+                                ws.data_ptr<float>(), (long long)ws.numel() * 4, stream_of(part)),
+           "vrvq_rvq_encode_part");
   return {codes, latents, loss_pf, z_q_is, z_q, mask};
 }
 
@@ -1085,12 +1162,12 @@ TORCH_LIBRARY(vrvq, m) {
   m.def(
       "snake_conv1d(Tensor x, Tensor w_packed, int cout, int stride, int pad, int dil, "
       "Tensor? bias, Tensor? alpha, Tensor? inv_alpha, Tensor? residual, int epilogue, "
-      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw, Tensor? w_x3=None, "
-      "bool ys_planes=False) -> (Tensor, Tensor)");
+      "Tensor? alpha_out, Tensor? inv_alpha_out, bool want_raw, Tensor? w_x3=None) "
+      "-> (Tensor, Tensor)");
   m.def(
       "snake_conv_transpose1d(Tensor x, Tensor w_packed, int cout, int stride, Tensor? bias, "
       "Tensor? alpha, Tensor? inv_alpha, Tensor? alpha_out, Tensor? inv_alpha_out, "
-      "bool want_raw, int pad=-1, Tensor? w_x3=None, bool ys_planes=False) -> (Tensor, Tensor)");
+      "bool want_raw, int pad=-1, Tensor? w_x3=None) -> (Tensor, Tensor)");
   m.def(
       "residual_unit(Tensor x, Tensor x_snk, int dil, Tensor w7, Tensor b7, Tensor alpha2, "
       "Tensor inv_alpha2, Tensor w1, Tensor b1, Tensor? alpha_out, Tensor? inv_alpha_out, "
@@ -1107,6 +1184,14 @@ TORCH_LIBRARY(vrvq, m) {
   m.def("rvq_pack_w_in(Tensor w_in_t) -> Tensor");
   m.def(
       "rvq_encode_fm(Tensor zt, Tensor w3in, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
+      "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
+      "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "snake_conv1d_proj(Tensor x, Tensor w_packed, int cout, int pad, int dil, Tensor? bias, "
+      "Tensor? alpha, Tensor? inv_alpha, Tensor? w_x3, Tensor w3in, int nq, bool want_z) "
+      "-> (Tensor, Tensor)");
+  m.def(
+      "rvq_encode_part(Tensor part, int frames, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
       "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
       "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("rvq_check_error(Tensor like, bool sync) -> int");
@@ -1170,6 +1255,8 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("snake_conv1d_fm", &snake_conv1d_fm); \
   m.impl("rvq_pack_w_in", &rvq_pack_w_in); \
   m.impl("rvq_encode_fm", &rvq_encode_fm); \
+  m.impl("snake_conv1d_proj", &snake_conv1d_proj); \
+  m.impl("rvq_encode_part", &rvq_encode_part); \
   m.impl("rvq_check_error", &rvq_check_error); \
   m.impl("rvq_gather", &rvq_gather); \
   m.impl("rvq_nearest", &rvq_nearest); \

@@ -73,6 +73,16 @@ class MPD(nn.Module):
                                     for ci, co, s in _MPD_LAYERS])
         self.conv_post = _wn(nn.Conv2d(1024, 1, (3, 1), padding=(1, 0)), False)
 
+    def to_reference_layout(self, fmap: torch.Tensor, batch: int) -> torch.Tensor:
+        """One map of forward() in the reference's (B, C, frames, period) layout (a view where
+        the folded layouts allow; the values are unchanged)."""
+        if fmap.dim() == 4:  # already the Conv2d form (VRVQ_MPD_1D=0)
+            return fmap
+        p = self.period
+        if MPD_GEMM:  # (B * p, frames, C)
+            return fmap.reshape(batch, p, fmap.shape[1], fmap.shape[2]).permute(0, 3, 2, 1)
+        return fmap.reshape(batch, p, fmap.shape[1], fmap.shape[2]).permute(0, 2, 3, 1)
+
     def forward(self, x):
         t = x.shape[-1]
         x = F.pad(x, (0, self.period - t % self.period), mode="reflect")
@@ -184,7 +194,15 @@ class MRD(nn.Module):
 class Discriminator(nn.Module):
     """MPD(periods) + MSD(rates) + MRD(fft_sizes) on peak-normalised, DC-removed audio
     (models/discriminator.py:178-220). forward(x) -> list (per discriminator) of feature maps,
-    the last one the logits."""
+    the last one the logits.
+
+    Feature-map layout: with VRVQ_MPD_1D / VRVQ_MPD_GEMM on (the default) each
+    period discriminator's maps are (B * period, frames, C) -- the channels-last folded batch its
+    GEMMs run on -- where the reference returns (B, C, frames, period). The values are the same
+    and every consumer in the training step (means, elementwise L1 between the real and the fake
+    maps: losses.GANLoss) is layout-invariant; a consumer that indexes the maps (hooks, per-layer
+    comparisons against reference fixtures) takes MPD.to_reference_layout(map, B) or runs with
+    VRVQ_MPD_1D=0 (the reference's Conv2d layout). MSD / MRD maps keep the reference layout."""
 
     def __init__(self, rates: List[int] = [], periods: List[int] = [2, 3, 5, 7, 11],
                  fft_sizes: List[int] = [2048, 1024, 512], sample_rate: int = 44100,

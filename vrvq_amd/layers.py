@@ -11,21 +11,12 @@ epilogue). Weight norm is folded once per parameter version, not per forward.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
 from . import ops
-
-
-# The residual units' k7 convs on the planes tile (csrc/conv_pl.h): their input snake(x) is
-# written as bf16 planes by the producing epilogue and staged by LDS-DMA. Off by default
-# (VRVQ_CONV_PLANES=1 turns it on): bit-identical, but slower over the step as measured --
-# the producers' planes epilogue costs more than the consumer saves (profiles/r05h_layers.txt:
-# 44.56 ms of convs vs 42.36 ms with fp32 snake(x) and the register-staged x3 tiles).
-PLANES = os.environ.get("VRVQ_CONV_PLANES", "0") == "1"
 
 
 def _param_key(*ps):
@@ -119,12 +110,9 @@ class WNConv1d(nn.Module):
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
                 residual: Optional[torch.Tensor] = None, epilogue: int = ops.EPI_NONE,
-                out_snake: Optional[Snake1d] = None, want_raw: bool = True,
-                ys_planes: bool = False):
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
         """conv(snake(x)) (+ residual, epilogue). With out_snake (the consumer's Snake1d)
-        returns (y or None, out_snake(y)) computed in the same epilogue; ys_planes: out_snake(y)
-        as bf16 planes for a planes k7 consumer. x may itself be such planes (snake(x) of a k7
-        conv, no snake here)."""
+        returns (y or None, out_snake(y)) computed in the same epilogue."""
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
@@ -134,7 +122,7 @@ class WNConv1d(nn.Module):
                           bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                           residual=residual, epilogue=epilogue,
                           out_snake=None if out_snake is None else out_snake.prepared(),
-                          want_raw=want_raw, w_x3=self.prepared_x3(), ys_planes=ys_planes)
+                          want_raw=want_raw, w_x3=self.prepared_x3())
 
 
     def forward_fm(self, x: torch.Tensor, snake: Optional[Snake1d] = None) -> torch.Tensor:
@@ -149,6 +137,22 @@ class WNConv1d(nn.Module):
         return ops.conv1d_fm(x, wp, self.out_channels, self.kernel_size[0], self.padding[0],
                              self.dilation[0], bias=self.bias.detach(), alpha=alpha,
                              inv_alpha=inv, w_x3=self.prepared_x3())
+
+    def forward_proj(self, x: torch.Tensor, w3in: torch.Tensor, nq: int,
+                     snake: Optional[Snake1d] = None, want_z: bool = False):
+        """conv(snake(x)) + bias (stride 1, 1024 outputs) with the in_proj of nq RVQ stages in
+        the epilogue (include/vrvq.h vrvq_conv1d_proj): returns (part, z or None), part the
+        (8, B*T, 8 nq) channel-split projection partials rvq_encode_part takes."""
+        if self.stride[0] != 1:
+            raise RuntimeError("forward_proj: stride-1 convs only")
+        wp, _ = self.prepared()
+        alpha = inv = None
+        if snake is not None:
+            alpha, inv = snake.prepared()
+        return ops.conv1d_proj(x, wp, self.out_channels, self.kernel_size[0], w3in, nq,
+                               self.padding[0], self.dilation[0], bias=self.bias.detach(),
+                               alpha=alpha, inv_alpha=inv, w_x3=self.prepared_x3(),
+                               want_z=want_z)
 
 
 class WNConvTranspose1d(nn.Module):
@@ -194,8 +198,7 @@ class WNConvTranspose1d(nn.Module):
         return self._cache_x3[1]
 
     def forward(self, x: torch.Tensor, snake: Optional[Snake1d] = None,
-                out_snake: Optional[Snake1d] = None, want_raw: bool = True,
-                ys_planes: bool = False):
+                out_snake: Optional[Snake1d] = None, want_raw: bool = True):
         wp, cout_pad = self.prepared()
         alpha = inv = None
         if snake is not None:
@@ -204,7 +207,7 @@ class WNConvTranspose1d(nn.Module):
                                     bias=self.bias.detach(), alpha=alpha, inv_alpha=inv,
                                     out_snake=None if out_snake is None else out_snake.prepared(),
                                     want_raw=want_raw, pad=self.padding[0],
-                                    w_x3=self.prepared_x3(), ys_planes=ys_planes)
+                                    w_x3=self.prepared_x3())
 
 
 class ResidualUnit(nn.Module):
@@ -236,14 +239,7 @@ class ResidualUnit(nn.Module):
         return self.fused and C in ops.RU_FUSED_CHANNELS and not (C == 256 and ops.X3 and
                                                                  ops.RU256_SPLIT)
 
-    def takes_planes(self) -> bool:
-        """The chained form's k7 conv runs on the planes tile (its producer then writes
-        block[0](x) as planes): two launches, x3 weights, C a multiple of 64 from 128."""
-        C = self.block[1].in_channels
-        return PLANES and ops.X3 and not self.runs_fused() and C % 64 == 0 and C >= 128
-
-    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool,
-            out_planes: bool = False):
+    def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool):
         """Chained form: x_snk = block[0](x) was produced by the previous layer's epilogue.
         For C in ops.RU_FUSED_CHANNELS one launch (vrvq_residual_unit: block[2](h) stays in
         LDS); otherwise the k7 conv writes only block[2](h) (h has no other consumer) and the
@@ -256,7 +252,7 @@ class ResidualUnit(nn.Module):
         # C = 256 with the x3 weights: the two launches (k7 on the x3 path at 128-row tiles,
         # then k1 + skip) beat the fused kernel, whose 256-row x3 weight stage does not fit
         # twice per CU and therefore keeps the fp32 MFMA (profiles/r02zi_bench_ab.txt)
-        if self.runs_fused() and x_snk.dtype != torch.int16 and not out_planes:
+        if self.runs_fused():
             w7, cp7 = self.block[1].prepared()
             w1, cp1 = self.block[3].prepared()
             a2, ia2 = self.block[2].prepared()
@@ -266,13 +262,11 @@ class ResidualUnit(nn.Module):
                                      out_snake=out_snake.prepared(), want_raw=want_raw,
                                      w7_x3=self.block[1].prepared_x3(),
                                      w1_x3=self.block[3].prepared_x3())
-        return self.run_two_launch(x, x_snk, out_snake, want_raw, out_planes)
+        return self.run_two_launch(x, x_snk, out_snake, want_raw)
 
-    def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool,
-                       out_planes: bool = False):
+    def run_two_launch(self, x, x_snk, out_snake: Snake1d, want_raw: bool):
         _, h_snk = self.block[1](x_snk, out_snake=self.block[2], want_raw=False)
-        return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw,
-                             ys_planes=out_planes)
+        return self.block[3](h_snk, residual=x, out_snake=out_snake, want_raw=want_raw)
 
 
 class EncoderBlock(nn.Module):
@@ -297,18 +291,13 @@ class EncoderBlock(nn.Module):
     def entry_snake(self) -> Snake1d:
         return self.block[0].block[0]
 
-    def takes_planes(self) -> bool:  # its first residual unit's k7 input
-        return self.block[0].takes_planes()
-
     def run(self, x: torch.Tensor, x_snk: torch.Tensor, out_snake: Optional[Snake1d],
-            want_raw: bool, out_planes: bool = False):
-        """Chained form (see ResidualUnit.run); returns what block[4] returns. out_planes: the
-        consumer of out_snake(y) takes bf16 planes (the next block's first k7)."""
+            want_raw: bool):
+        """Chained form (see ResidualUnit.run); returns what block[4] returns."""
         for i in range(3):
             nxt = self.block[i + 1].block[0] if i < 2 else self.block[3]
-            planes = i < 2 and self.block[i + 1].takes_planes()
-            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=i < 2, out_planes=planes)
-        return self.block[4](x_snk, out_snake=out_snake, want_raw=want_raw, ys_planes=out_planes)
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=i < 2)
+        return self.block[4](x_snk, out_snake=out_snake, want_raw=want_raw)
 
 
 class DecoderBlock(nn.Module):
@@ -337,12 +326,9 @@ class DecoderBlock(nn.Module):
     def run(self, x_snk: torch.Tensor, out_snake: Snake1d, want_raw: bool = False):
         """Chained form: x_snk = block[0](x) from the previous epilogue; returns
         (y or None, out_snake(y))."""
-        x, x_snk = self.block[1](x_snk, out_snake=self.block[2].block[0], want_raw=True,
-                                 ys_planes=self.block[2].takes_planes())
+        x, x_snk = self.block[1](x_snk, out_snake=self.block[2].block[0], want_raw=True)
         for i in range(2, 5):
             last = i == 4
             nxt = out_snake if last else self.block[i + 1].block[0]
-            planes = (not last) and self.block[i + 1].takes_planes()
-            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=want_raw if last else True,
-                                         out_planes=planes)
+            x, x_snk = self.block[i].run(x, x_snk, nxt, want_raw=want_raw if last else True)
         return x, x_snk

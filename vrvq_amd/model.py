@@ -34,10 +34,13 @@ class Encoder(nn.Module):
         self.block = nn.Sequential(*blocks)
         self.valid = False  # padding=False (CodecMixin.padding): unpadded convs
 
-    def forward(self, x, return_feat: bool = False, frame_major: bool = False):
+    def forward(self, x, return_feat: bool = False, frame_major: bool = False,
+                project: Optional["_Stacked"] = None):
         """frame_major: z comes back as the (B, D, T) view of a frame-major (B, T, D) tensor,
         written that way by the last conv's epilogue (the layout the fused RVQ reads, see
-        _is_frame_major); the values are the same."""
+        _is_frame_major); the values are the same. project (a quantizer's stacked stage
+        weights): z comes back as a ProjectedZ -- the last conv's epilogue projects it onto every
+        stage's in_proj (include/vrvq.h vrvq_conv1d_proj) and z itself is not written."""
         if self.training:  # autograd path (vrvq_amd/train.py)
             if self.valid:
                 raise NotImplementedError("padding=False is an inference (compress) mode")
@@ -62,11 +65,15 @@ class Encoder(nn.Module):
         for i in range(1, n - 2):
             last = i == n - 3
             nxt = None if last else self.block[i + 1].entry_snake()
-            planes = (not last) and self.block[i + 1].takes_planes()
-            r = self.block[i].run(x, x_snk, nxt, want_raw=True, out_planes=planes)
+            r = self.block[i].run(x, x_snk, nxt, want_raw=True)
             x, x_snk = (r, None) if last else r
         feat = x  # output of block index n-3 (the last EncoderBlock), models/dac_vrvq.py:43-44
-        if frame_major:
+        if project is not None:
+            nq = project.b_in.shape[0]
+            part, _ = self.block[n - 1].forward_proj(x, project.w3in(), nq, snake=self.block[n - 2])
+            B = x.shape[0]
+            out = ProjectedZ(part, B, self.block[n - 1].out_channels, part.shape[1] // B, nq)
+        elif frame_major:
             out = self.block[n - 1].forward_fm(x, snake=self.block[n - 2]).transpose(1, 2)
         else:
             out = self.block[n - 1](x, snake=self.block[n - 2])
@@ -161,10 +168,32 @@ class VectorQuantize(nn.Module):
         return z_q, loss, loss.clone(), codes[:, 0, :], latents
 
 
-# The encoder hands z to the quantizer frame-major (vrvq_rvq_encode_fm: each chain part reads
-# its frames' contiguous rows and projects them itself) unless VRVQ_RVQ_FM=0 (A/B: z (B, D, T)
-# and vrvq_rvq_encode).
+# The eval encode hands z to the quantizer as its stage projections: the encoder's last conv
+# computes every stage's in_proj in its epilogue (vrvq_conv1d_proj) and the quantizer runs from
+# those partials (vrvq_rvq_encode_part: no z read, no projection in front of the chain).
+# VRVQ_RVQ_PROJ=0 (A/B): z frame-major and vrvq_rvq_encode_fm (chain parts project their own
+# frames), or, with VRVQ_RVQ_FM=0 as well, z (B, D, T) and vrvq_rvq_encode.
+RVQ_PROJ = os.environ.get("VRVQ_RVQ_PROJ", "1") != "0"
 RVQ_FM = os.environ.get("VRVQ_RVQ_FM", "1") != "0"
+
+
+class ProjectedZ:
+    """The encoder's z as the eval quantizer consumes it: the in_proj of every stage, computed in
+    the last conv's epilogue (include/vrvq.h vrvq_conv1d_proj) as (8, B*T, 8 nq) channel-split
+    partials -- rvq_project's values bit for bit. z (B, D, T) itself is not materialised; `shape`
+    is its shape."""
+
+    def __init__(self, part: torch.Tensor, B: int, D: int, T: int, nq: int):
+        self.part = part
+        self.shape = torch.Size((B, D, T))
+        self.nq = nq
+
+    def dim(self) -> int:
+        return 3
+
+    @property
+    def device(self):
+        return self.part.device
 
 
 def _is_frame_major(z: torch.Tensor) -> bool:
@@ -173,7 +202,14 @@ def _is_frame_major(z: torch.Tensor) -> bool:
 
 
 def _rvq_encode(z, st, **kw):
-    """ops.rvq_encode, or ops.rvq_encode_fm when z is a frame-major view."""
+    """ops.rvq_encode_part for a ProjectedZ, ops.rvq_encode_fm when z is a frame-major view,
+    else ops.rvq_encode."""
+    if isinstance(z, ProjectedZ):
+        if z.nq != st.b_in.shape[0]:
+            raise RuntimeError(f"ProjectedZ holds {z.nq} stages' projections, the quantizer "
+                               f"runs {st.b_in.shape[0]}")
+        return ops.rvq_encode_part(z.part, z.shape[2], st.b_in, st.cb, st.cbf, st.c2, st.w_out,
+                                   st.b_out, st.mcol, st.qb, **kw)
     if _is_frame_major(z):
         return ops.rvq_encode_fm(z.transpose(1, 2), st.w3in(), st.b_in, st.cb, st.cbf, st.c2,
                                  st.w_out, st.b_out, st.mcol, st.qb, **kw)
@@ -536,8 +572,16 @@ class DAC_VRVQ(nn.Module, CodecMixin):
         `want_z_q_is=False` skips materialising the (B, Nq, D, T) per-codebook tensor when the
         caller does not need it (it is ~90 % of the quantizer's HBM traffic); the default keeps
         the reference's dict."""
-        fm = RVQ_FM and not self.training and not self.encoder.valid
-        z, feat = self.encoder(audio_data.contiguous(), return_feat=True, frame_major=fm)
+        ev = not self.training and not self.encoder.valid
+        # the projection epilogue serves every stage: not a CBR prefix (n_quantizers < Nq)
+        proj = RVQ_PROJ and ev and (self.model_type == "VBR" or n_quantizers is None
+                                    or int(n_quantizers) >= self.n_codebooks)
+        if proj:
+            z, feat = self.encoder(audio_data.contiguous(), return_feat=True,
+                                   project=self.quantizer.stacked())
+        else:
+            z, feat = self.encoder(audio_data.contiguous(), return_feat=True,
+                                   frame_major=RVQ_FM and ev)
         if self.model_type == "CBR":
             return self.quantizer(z, n_quantizers)
         return self.quantizer(z, n_quantizers, feat, level, want_z_q_is=want_z_q_is)

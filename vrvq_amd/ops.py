@@ -99,21 +99,19 @@ def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k:
            alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, epilogue: int = EPI_NONE,
            out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, want_raw: bool = True,
-           w_x3: Optional[torch.Tensor] = None, ys_planes: bool = False):
+           w_x3: Optional[torch.Tensor] = None):
     """y = epi(residual + conv1d(snake(x)) + bias) on the MFMA implicit-GEMM kernel.
 
     out_snake = (alpha_next, inv_alpha_next) also produces snake_next(y) from the epilogue
     (the next layer's Snake). Returns y, or (y | None, snake_next(y)) when out_snake is given
     (y is None when want_raw is False). w_x3 = pack_x3_weight(w_packed, k) selects the bf16x3
-    split MFMA path for stride-1 convs (include/vrvq.h). ys_planes: snake_next(y) comes back as
-    bf16 planes (B, 3, Cout/8, T, 8) int16, the input layout of the k7 planes tile; x may be such
-    a planes tensor (snake(x) for a k7 conv, alpha None: include/vrvq.h vrvq_conv1d_ex)."""
+    split MFMA path for stride-1 convs (include/vrvq.h)."""
     if w_packed.dim() != 3 or w_packed.shape[1] != k or w_packed.shape[2] != cout_pad:
         raise RuntimeError("conv1d: w_packed must be (Cin, k, cout_pad)")
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv1d(x, w_packed, int(cout), int(stride), int(pad), int(dil), bias,
                                 alpha, inv_alpha, residual, int(epilogue), ao, io, bool(want_raw),
-                                w_x3, bool(ys_planes))
+                                w_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -129,19 +127,33 @@ def conv1d_fm(x: torch.Tensor, w_packed: torch.Tensor, cout: int, k: int, pad: i
                                   inv_alpha, w_x3)
 
 
+def conv1d_proj(x: torch.Tensor, w_packed: torch.Tensor, cout: int, k: int, w3in: torch.Tensor,
+                nq: int, pad: int = 0, dil: int = 1, bias: Optional[torch.Tensor] = None,
+                alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
+                w_x3: Optional[torch.Tensor] = None, want_z: bool = False):
+    """conv1d(snake(x)) + bias (stride 1, cout 1024: the encoder's last conv) with the in_proj of
+    all nq RVQ stages in its epilogue (include/vrvq.h vrvq_conv1d_proj). Returns (part, z):
+    part (8, B*T, 8 nq) = rvq_project's channel-split partials, bit for bit, and z (B, 1024, T)
+    when want_z (else None). w3in = rvq_pack_w_in(w_in_t)."""
+    if w_packed.dim() != 3 or w_packed.shape[1] != k:
+        raise RuntimeError("conv1d_proj: w_packed must be (Cin, k, cout_pad)")
+    part, z = _ops().snake_conv1d_proj(x, w_packed, int(cout), int(pad), int(dil), bias, alpha,
+                                       inv_alpha, w_x3, w3in, int(nq), bool(want_z))
+    return part, _none(z)
+
+
 def conv_transpose1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int,
                      stride: int, bias: Optional[torch.Tensor] = None,
                      alpha: Optional[torch.Tensor] = None,
                      inv_alpha: Optional[torch.Tensor] = None,
                      out_snake: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                      want_raw: bool = True, pad: int = -1,
-                     w_x3: Optional[torch.Tensor] = None, ys_planes: bool = False):
+                     w_x3: Optional[torch.Tensor] = None):
     """Polyphase ConvTranspose1d (k = 2*stride); out_snake / want_raw as in conv1d. pad -1 is
     the DecoderBlock's ceil(stride / 2), 0 the padding=False window of the chunked codec."""
     ao, io = out_snake if out_snake is not None else (None, None)
     y, ys = _ops().snake_conv_transpose1d(x, w_packed, int(cout), int(stride), bias, alpha,
-                                          inv_alpha, ao, io, bool(want_raw), int(pad), w_x3,
-                                          bool(ys_planes))
+                                          inv_alpha, ao, io, bool(want_raw), int(pad), w_x3)
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
@@ -234,6 +246,18 @@ def rvq_encode_fm(zt, w3in, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
     codes, lat, loss, zqis, zq, mask = _ops().rvq_encode_fm(zt, w3in, b_in, cb, cbf, c2, w_out,
                                                           b_out, mcol, qb, imp, float(level),
                                                           bool(want_z_q_is), bool(want_mask))
+    return codes, lat, loss, _none(zqis), zq, _none(mask)
+
+
+def rvq_encode_part(part, frames, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
+                    level: float = 1.0, want_z_q_is: bool = True, want_mask: bool = True):
+    """rvq_encode from conv1d_proj's partials (8, B*T, 8 nq): one launch per group of resident
+    clips (include/vrvq.h vrvq_rvq_encode_part), or the chain + expansion launches where a clip
+    does not fit it. Same outputs as rvq_encode's three launches, bit for bit."""
+    codes, lat, loss, zqis, zq, mask = _ops().rvq_encode_part(part, int(frames), b_in, cb, cbf,
+                                                            c2, w_out, b_out, mcol, qb, imp,
+                                                            float(level), bool(want_z_q_is),
+                                                            bool(want_mask))
     return codes, lat, loss, _none(zqis), zq, _none(mask)
 
 
@@ -393,25 +417,19 @@ def _register_fakes():
         y = f32(x, shape) if (want_raw or ao is None) else none(x)
         return y, ys
 
-    def planes(x, B, C, T):
-        return x.new_empty((B, 3, C // 8, T, 8), dtype=torch.int16)
-
     @reg("vrvq::snake_conv1d")
     def _(x, w_packed, cout, stride, pad, dil, bias, alpha, inv_alpha, residual, epilogue,
-          alpha_out, inv_alpha_out, want_raw, w_x3=None, ys_planes=False):
-        B = x.shape[0]
-        tin = x.shape[3] if x.dim() == 5 else x.shape[2]
+          alpha_out, inv_alpha_out, want_raw, w_x3=None):
+        B, _c, tin = x.shape
         tout = conv_out_len(tin, w_packed.shape[1], stride, pad, dil)
-        y, ys = pair(x.new_empty((1,), dtype=torch.float32), (B, cout, tout), alpha_out, want_raw)
-        return y, planes(x, B, cout, tout) if ys_planes else ys
+        return pair(x, (B, cout, tout), alpha_out, want_raw)
 
     @reg("vrvq::snake_conv_transpose1d")
     def _(x, w_packed, cout, stride, bias, alpha, inv_alpha, alpha_out, inv_alpha_out, want_raw,
-          pad=-1, w_x3=None, ys_planes=False):
+          pad=-1, w_x3=None):
         B, _c, tin = x.shape
         tout = convt_out_len(tin, stride, pad)
-        y, ys = pair(x, (B, cout, tout), alpha_out, want_raw)
-        return y, planes(x, B, cout, tout) if ys_planes else ys
+        return pair(x, (B, cout, tout), alpha_out, want_raw)
 
     @reg("vrvq::residual_unit")
     def _(x, x_snk, dil, w7, b7, alpha2, inv_alpha2, w1, b1, alpha_out, inv_alpha_out, want_raw,
@@ -454,6 +472,23 @@ def _register_fakes():
         return (zt.new_empty((B, nq, T), dtype=torch.int64), f32(zt, (B, nq * d, T)),
                 f32(zt, (B, nq, T)), f32(zt, (B, nq, D, T)) if want_z_q_is else none(zt),
                 f32(zt, (B, D, T)), f32(zt, (B, nq, T)) if want_mask else none(zt))
+
+    @reg("vrvq::snake_conv1d_proj")
+    def _(x, w_packed, cout, pad, dil, bias, alpha, inv_alpha, w_x3, w3in, nq, want_z):
+        B, _c, tin = x.shape
+        T = conv_out_len(tin, w_packed.shape[1], 1, pad, dil)
+        return f32(x, (8, B * T, nq * 8)), (f32(x, (B, cout, T)) if want_z else none(x))
+
+    @reg("vrvq::rvq_encode_part")
+    def _(part, frames, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp, level, want_z_q_is,
+          want_mask):
+        T = frames
+        B = part.shape[1] // T
+        nq, _n, d = cb.shape
+        D = w_out.shape[1]
+        return (part.new_empty((B, nq, T), dtype=torch.int64), f32(part, (B, nq * d, T)),
+                f32(part, (B, nq, T)), f32(part, (B, nq, D, T)) if want_z_q_is else none(part),
+                f32(part, (B, D, T)), f32(part, (B, nq, T)) if want_mask else none(part))
 
     @reg("vrvq::rvq_gather")
     def _(codes, cb):

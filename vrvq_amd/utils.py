@@ -58,6 +58,22 @@ def masked_sum(z_q_is: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return ops.masked_sum(z_q_is.contiguous(), mask.contiguous())
 
 
+def check_errors(device=None) -> None:
+    """End-of-work check for the fused RVQ launches' bounded in-kernel waits (include/vrvq.h
+    vrvq_rvq_pending_error): synchronises the device, then raises RuntimeError if any launch
+    completed by now timed out (its outputs were poisoned: codes -1, NaN z_q). The RVQ ops also
+    raise on such a code at their next call; a one-shot caller (a single encode, the last call of
+    a sweep) calls this after its own work instead. Clears the code it reports."""
+    from . import _lib
+    torch.cuda.synchronize(device)
+    code = _lib.rvq_pending_error()
+    if code:
+        raise RuntimeError(
+            f"vrvq: a fused RVQ launch timed out in an in-kernel hand-off (code {code}: "
+            f"{'projection partials' if code == 1 else 'stage rows'}); its outputs are invalid "
+            "(codes -1, NaN)")
+
+
 def sweep_latents(imp_map: torch.Tensor, z_q_is: torch.Tensor, levels: Sequence[float],
                   n_q: int):
     """Per level: hard mask of imp_map * (level * Nq) and the masked sum of z_q_is
@@ -90,6 +106,7 @@ def level_sweep(model, audio: torch.Tensor, levels: Sequence[float], bits_per_co
                 raise ValueError("max_decode_clips must be >= 1")
             recon_all = torch.cat([model.decode(z_all[i:i + cap])
                                    for i in range(0, z_all.shape[0], cap)])
+    check_errors(audio.device)  # the sweep's one encode: a timed-out hand-off raises here
     B = audio.shape[0]
     out = []
     for li, level in enumerate(levels):
