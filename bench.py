@@ -50,7 +50,7 @@ SR = 44100
 LEVELS = (0.25, 0.5, 1.0, 2.0)
 # the reference inference driver's own sweep (scripts/inference.py:58-70: 10-s clips, 12 levels)
 LEVELS_INFERENCE = (0.2, 0.3, 0.4, 0.5, 0.6, 0.8, 1.0, 1.2, 1.5, 2.0, 2.5, 3.0)
-RVQ_KERNELS = ("rvq_pt_kernel", "rvq_fm_kernel", "rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
+RVQ_KERNELS = ("rvq_pt_kernel", "rvq_fused_kernel", "rvq_project3_kernel", "rvq_project2_kernel",
                "rvq_chain_kernel", "rvq_expand_kernel")
 
 
@@ -191,10 +191,9 @@ class RvqTimer:
                 return r
             return timed
         # the eval encode's entry (from the conv's partials, model.py RVQ_PROJ) and the
-        # frame-major / channel-major ones of the A/B paths
+        # channel-major one of the A/B path (VRVQ_RVQ_PROJ=0)
         ops.rvq_encode_part = wrap(ops.rvq_encode_part)
         ops.rvq_encode = wrap(ops.rvq_encode)
-        ops.rvq_encode_fm = wrap(ops.rvq_encode_fm)
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -518,8 +517,9 @@ def main(argv=None):
                                     "chain; expansion workgroups with a loader wave write z_q_is "
                                     "/ z_q; in-launch tagged-granule hand-offs)"
                                     if from_part else
-                                    "RVQ path: one torch.ops.vrvq.rvq_encode_fm = rvq_fm_kernel "
-                                    "per <= 32 clips (A/B path, VRVQ_RVQ_PROJ=0)"),
+                                    "RVQ path: torch.ops.vrvq.rvq_encode on channel-major z = "
+                                    "rvq_fused_kernel per <= 32 clips at T <= 96, else three "
+                                    "launches (A/B path, VRVQ_RVQ_PROJ=0)"),
                          "bytes_per_call": byt,
                          "bytes_model": ("SURVEY.md §8(d) with the kernel's input = the 8 "
                                          "channel-split in_proj partials (8 x 8 nq fp32 per "

@@ -107,15 +107,6 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
-/* vrvq_conv1d (stride 1, no residual / epilogue / output Snake) writing y FRAME-MAJOR:
- * y_fm[b][t][co] (tout x cout per clip, cout % 4 == 0, 16-byte aligned) -- the encoder's last
- * conv (models/dac_vrvq.py:34) producing z in the layout of vrvq_rvq_encode_fm's zt, straight
- * from the MFMA accumulators (no transpose pass). Same values as vrvq_conv1d's y. */
-int vrvq_conv1d_fm(const float* x, int batch, int cin, int tin, const float* alpha,
-                   const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
-                   int cout_pad, int k, int pad, int dil, const float* bias, float* y_fm,
-                   int tout, vrvq_stream_t stream);
-
 /* fp32 convolution on the bf16 matrix cores (the "x3" path, vrvq_amd/csrc/conv_x3.h): with
  * w_x3 = vrvq_pack_x3_weight(w_packed) (null: the fp32-input MFMA path) the stride-1 convs
  * (k in {1, 2, 3, 7}; also the ConvTranspose1d and the ResidualUnit's k7) split both operands
@@ -244,21 +235,22 @@ int vrvq_rvq_frag(const float* cbn, int nq, int ncode, int cdim, float* cbf,
 /* Projection kernel used by vrvq_rvq_project / vrvq_rvq_encode (both launch structures,
  * process-wide): 3 = one workgroup per clip x channel split on the bf16 matrix cores with both
  * operands split exactly into three bf16 terms (six products, fp32 accuracy; default); 2 = the
- * same unit on the fp32-input MFMA; 1 = 48-frame tiles x 64-row blocks (fp32). 1 and 2 write the
- * same partials bit for bit; 3 agrees with them to fp32 rounding (A/B timing; also
- * VRVQ_RVQ_PROJECT=1 / 2 in the environment). variant 0 queries. Returns the previous variant
- * (1, 2 or 3), or VRVQ_ERR_ARG. */
+ * same unit on the fp32-input MFMA (an exact fmaf chain per split: the exactness fallback; also
+ * VRVQ_RVQ_PROJECT=2 in the environment). 3 agrees with 2 to fp32 rounding. variant 0 queries.
+ * Returns the previous variant (2 or 3), or VRVQ_ERR_ARG. */
 int vrvq_rvq_project_variant(int variant);
 
 /* Bytes of the workspace vrvq_rvq_encode needs (projection partials + straight-through rows /
  * the fused launch's stage hand-off rows, whichever is larger). */
 int vrvq_rvq_workspace(int batch, int frames, int nq, long long* bytes);
 
-/* RVQ launch structure of vrvq_rvq_encode (process-wide): 2 = ONE fused launch where the shape
- * allows it (frames <= 96; up to 32 clips per launch, more clips run as consecutive launches),
- * else three launches (default); 1 = always the three launches (also VRVQ_RVQ_FUSED=0 in the
- * environment). Both give the same outputs bit for bit. path 0 queries. Returns the previous
- * path (1 or 2), or VRVQ_ERR_ARG. */
+/* RVQ launch structure (process-wide): 2 = fused launches (default): vrvq_rvq_encode runs ONE
+ * fused launch where the shape allows it (frames <= 96; up to 32 clips per launch, more clips
+ * run as consecutive launches), else its three launches; vrvq_rvq_encode_part runs rvq_pt_kernel
+ * per group of resident clips. 1 = never fused: vrvq_rvq_encode's three launches,
+ * vrvq_rvq_encode_part's two (chain, expansion); also VRVQ_RVQ_FUSED=0 in the environment.
+ * Every structure gives the same outputs bit for bit. path 0 queries. Returns the previous path
+ * (1 or 2), or VRVQ_ERR_ARG. */
 int vrvq_rvq_path(int path);
 
 /* The fused launches' in-kernel waits are bounded. A wait that runs out (a hang averted: it
@@ -284,30 +276,11 @@ int vrvq_rvq_debug(unsigned spin_max, unsigned stall);
 int vrvq_rvq_timing(int on);
 int vrvq_rvq_timing_read(float* mean_ms, int* count);
 
-/* The whole quantizer from FRAME-MAJOR z: zt[b][t][c] (B x T x D; vrvq_conv1d_fm writes it).
- * ONE launch per group of resident clips, any T: each chain part (<= 16 frames of a clip)
- * projects its own frames (its zt rows are contiguous: no line amplification, no partial
- * hand-off between workgroups) on the bf16 matrix cores with the exact three-term split of both
- * operands (fp32 accuracy), runs the 8-dim chain and publishes every stage's zst rows; expansion
- * workgroups (clip, 128 frames, 128 channels) write z_q_is / z_q under the chain. Outputs, layouts
- * and expressions as vrvq_rvq_encode. w3in = vrvq_rvq_pack_w_in(w_in_t) (once per weight
- * version, vrvq_rvq_w_in_planes_size uint16 elements). Hand-off granules: eager calls use a
- * library-owned area per (device, stream) (workspace may be NULL); under stream capture pass a
- * workspace of >= vrvq_rvq_workspace_fm bytes (zeroed by captured memsets; its first 8448 bytes
- * are then the launch's sync block, word 2048 its wait status -- vrvq_rvq_sync_error covers
- * eager calls only; the host-mapped word of vrvq_rvq_pending_error covers both). VRVQ_ERR_UNSUPPORTED
- * when the shape does not fit the launch (the caller then transposes and takes
- * vrvq_rvq_encode). Replaces models/quantize.py:353-365, 389-421 like vrvq_rvq_encode. */
+/* W_in planes of vrvq_conv1d_proj's projection epilogue (once per weight version,
+ * vrvq_rvq_w_in_planes_size uint16 elements): the three bf16 terms of W_in in the
+ * v_mfma_f32_16x16x32_bf16 A-fragment order. */
 int vrvq_rvq_w_in_planes_size(int nq, int dim, int cdim, long long* n_u16);
 int vrvq_rvq_pack_w_in(const float* w_in_t, int nq, int dim, int cdim, uint16_t* w3in,
-                       vrvq_stream_t stream);
-int vrvq_rvq_workspace_fm(int batch, int frames, int nq, int ncode, long long* bytes);
-int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frames, int nq, int ncode,
-                       int cdim, const uint16_t* w3in, const float* b_in, const float* cb,
-                       const float* cbf, const float* c2, const float* w_out, const float* b_out,
-                       const float* mcol, const float* qb, const float* imp, float level,
-                       int64_t* codes, float* latents, float* loss_pf, float* z_q_is, float* z_q,
-                       float* mask, void* workspace, long long workspace_bytes,
                        vrvq_stream_t stream);
 
 /* The whole quantizer from the projection partials of vrvq_conv1d_proj (the eval encode's path):

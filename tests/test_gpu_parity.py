@@ -655,9 +655,10 @@ def test_rvq_encode_vs_fp64(nq, ncode, B, T, vbr):
 @pytest.mark.parametrize("nq,B,T", [(8, 32, 87), (32, 64, 87), (28, 3, 70), (1, 4, 87), (5, 3, 40),
                                     (9, 2, 200), (2, 1, 1), (12, 2, 97)])
 def test_rvq_projection_variants_bit_identical(nq, B, T):
-    """The fp32 clip x split projection kernel and the 48-frame-tile kernel write the same
-    partials: every output of rvq_encode is bit-identical between them (odd nq, partial frame
-    tiles, T > 96, one frame, full config-2/3 batches). The split-bf16 kernel (variant 3, the
+    """The fp32-input projection (variant 2, the exactness fallback) gives every output of
+    rvq_encode bit-identical between the three launches and the fused launch that embeds the
+    same projection body (odd nq, partial frame tiles, T > 96 -- the fused path then takes the
+    three launches --, one frame, full config-2/3 batches). The split-bf16 kernel (variant 3, the
     default) agrees to fp32 rounding: codes vs fp64 in test_rvq_encode_vs_fp64 and the fixtures,
     z_q_is here within 1e-6."""
     from vrvq_amd import _lib
@@ -666,12 +667,12 @@ def test_rvq_projection_variants_bit_identical(nq, B, T):
     z = (torch.randn(B, 1024, T, generator=gen) * 0.3).to(DEV)
     imp = torch.rand(B, T, generator=gen).to(DEV)
     outs = {}
-    prev = _lib.rvq_project_variant(0)
-    prev_path = _lib.rvq_path(1)  # the three launches: the variants are their first kernel
+    prev = _lib.rvq_project_variant(2)
+    prev_path = _lib.rvq_path(0)
     try:
-        for v in (1, 2):
-            _lib.rvq_project_variant(v)
-            outs[v] = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=0.8)
+        for path in (1, 2):
+            _lib.rvq_path(path)
+            outs[path] = ops.rvq_encode(z, *st.codes_args(), imp=imp, level=0.8)
             torch.cuda.synchronize()
     finally:
         _lib.rvq_project_variant(prev)

@@ -6,7 +6,7 @@ fit the resident grid). Needs an MI355X.
 Bar: BIT-IDENTICAL to the three-launch path (vrvq_rvq_project's x3 partials -> chain ->
 expansion, vrvq_rvq_path(1)) on every output -- the partials are that projection's values and the
 chain sums them in the same split order -- hence codes / masks exact and z_q / z_q_is within the
-three-launch path's own tolerance against fp64 (test_gpu_parity.py, test_gpu_rvq_fm.py);
+three-launch path's own tolerance against fp64 (test_gpu_parity.py);
 reference fixtures pin DAC_VRVQ.encode on this path in test_gpu_parity.py."""
 import ctypes
 
@@ -192,6 +192,61 @@ def test_rvq_part_graph_replay_and_streams():
         _equal(o, want)
 
 
+def test_rvq_part_launch_counts():
+    """The fused launch really runs (a 0-capacity occupancy answer would silently
+    select another path): one timed launch per call at configs[1], at least one at the configs[2]
+    shape (B = 64 x nq = 32)."""
+    for nq, B, want_launches in ((8, 32, 1), (32, 64, None)):
+        q, gen = _random_rvq(nq, 1024, 5 + nq)
+        st = q.stacked()
+        z = (torch.randn(B, 1024, 87, generator=gen) * 0.3).to(DEV)
+        part = _project(z, st)
+        _part_call(part, 87, st, None, 1.0)
+        torch.cuda.synchronize()
+        _lib.rvq_timing_read()
+        prev = _lib.rvq_timing(True)
+        try:
+            _part_call(part, 87, st, None, 1.0)
+            torch.cuda.synchronize()
+            ms, n = _lib.rvq_timing_read()
+        finally:
+            _lib.rvq_timing(prev)
+        assert n >= 1 and ms > 0.0
+        if want_launches is not None:
+            assert n == want_launches
+
+
+def test_rvq_fused_timeout_is_loud():
+    """rvq_encode's fused launch on channel-major z: a hand-off wait that runs out (waits bounded
+    at 64 polls, the first projection unit held back) poisons its outputs (codes -1 or NaN z_q)
+    and the NEXT RVQ call raises RuntimeError without any synchronisation in between; after the
+    knob is reset a clean call succeeds and reports nothing."""
+    q, gen = _random_rvq(8, 1024, 31)
+    st = q.stacked()
+    z = (torch.randn(4, 1024, 87, generator=gen) * 0.3).to(DEV)
+    run = lambda: ops.rvq_encode(z, *st.codes_args(), level=1.0)  # noqa: E731
+    prev = _lib.rvq_path(2)
+    try:
+        ref = run()
+        torch.cuda.synchronize()
+        _lib.rvq_debug(spin_max=64, stall=400)
+        bad = run()
+        torch.cuda.synchronize()
+        _lib.rvq_debug(0, 0)
+        assert bool((bad[0] < 0).any()) or bool(torch.isnan(bad[4]).any())
+        with pytest.raises(RuntimeError, match="timed out"):
+            run()
+        torch.cuda.synchronize()
+        assert ops.rvq_check_error(z, sync=True) in (0, 1, 2)  # drained
+        good = run()
+        torch.cuda.synchronize()
+        assert ops.rvq_check_error(z, sync=True) == 0
+        assert torch.equal(good[0], ref[0]) and torch.equal(good[4], ref[4])
+    finally:
+        _lib.rvq_debug(0, 0)
+        _lib.rvq_path(prev)
+
+
 def test_rvq_part_timeout_is_loud_for_a_one_shot_caller():
     """A hand-off wait that runs out (waits bounded at 64 polls, the first chain part held back)
     poisons the outputs, and a ONE-SHOT caller learns it from vrvq_amd.check_errors() (RuntimeError
@@ -218,7 +273,7 @@ def test_rvq_part_timeout_is_loud_for_a_one_shot_caller():
 
 def test_encode_projected_matches_channel_major(manifest):
     """DAC_VRVQ.encode on the default path (projection epilogue + rvq_encode_part) against the
-    channel-major z path (VRVQ_RVQ_PROJ=0, VRVQ_RVQ_FM=0: rvq_encode) -- every output of the dict
+    channel-major z path (VRVQ_RVQ_PROJ=0: rvq_encode) -- every output of the dict
     bit for bit -- and against itself with the fused launch's capacity forced to 0 (the two-launch
     fallback a clip too long for the grid takes)."""
     from test_gpu_parity import model_for, t
@@ -229,12 +284,11 @@ def test_encode_projected_matches_channel_major(manifest):
     m = vrvq_amd.model
     with torch.no_grad():
         a = model.encode(x, level=1.0)
-        prev = (m.RVQ_PROJ, m.RVQ_FM)
-        m.RVQ_PROJ, m.RVQ_FM = False, False
+        prev, m.RVQ_PROJ = m.RVQ_PROJ, False
         try:
             b = model.encode(x, level=1.0)
         finally:
-            m.RVQ_PROJ, m.RVQ_FM = prev
+            m.RVQ_PROJ = prev
         prev_c = _lib.rvq_debug_capacity(0)
         try:
             c = model.encode(x, level=1.0)
@@ -247,3 +301,24 @@ def test_encode_projected_matches_channel_major(manifest):
             continue
         assert torch.equal(a[key], b[key]), key
         assert torch.equal(a[key], c[key]), key
+
+
+def test_encode_cbr_prefix_projected_matches_channel_major():
+    """A CBR model's encode with n_quantizers < Nq projects only the prefix's stages in the conv
+    epilogue (the stacked prefix, cached per n): the dict equals the channel-major z path's bit
+    for bit, for several prefixes and the full set."""
+    model = vrvq_amd.DAC_VRVQ(n_codebooks=8, model_type="CBR").to(DEV).eval()
+    gen = torch.Generator().manual_seed(5)
+    x = model.preprocess((torch.rand(2, 1, 44100, generator=gen) * 2 - 1).to(DEV), 44100)
+    m = vrvq_amd.model
+    with torch.no_grad():
+        for n in (1, 4, 7, 8, None):
+            a = model.encode(x, n)
+            prev, m.RVQ_PROJ = m.RVQ_PROJ, False
+            try:
+                b = model.encode(x, n)
+            finally:
+                m.RVQ_PROJ = prev
+            torch.cuda.synchronize()
+            for key in a:
+                assert (a[key] is None and b[key] is None) or torch.equal(a[key], b[key]), (n, key)

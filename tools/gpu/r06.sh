@@ -15,17 +15,17 @@ has() { [[ " $STEPS " == *" $1 "* ]]; }
 PT="python -u -m pytest -x -q -rf --timeout 120 --timeout-method thread"
 has smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has pt && run pt_tests 600 $PT tests/test_gpu_rvq_part.py
-has fm && run fm_tests 500 $PT tests/test_gpu_rvq_fm.py
+
 has rvqtests && run rvq_tests 700 $PT tests/test_gpu_parity.py -k "rvq or golden or model_forward or config or sweep or batch or ragged or deterministic or cbr"
 has convtests && run conv_tests 600 $PT tests/test_gpu_parity.py -k "conv or strided or transpose or residual or model_forward or x3"
 has long && run long_tests 500 $PT tests/test_gpu_long_clip.py
-has rvqb && run rvq_b32 180 python tools/rvq_bench.py --batch 32 --nq 8 --variants 3 --paths pt,fm,1
-has rvqb && run rvq_b64 180 python tools/rvq_bench.py --batch 64 --nq 32 --variants 3 --paths pt,fm
-has rvqb10 && run rvq_b1x10 180 python tools/rvq_bench.py --batch 1 --frames 862 --nq 8 --variants 3 --paths pt,fm
+has rvqb && run rvq_b32 180 python tools/rvq_bench.py --batch 32 --nq 8 --variants 3 --paths pt,2,1
+has rvqb && run rvq_b64 180 python tools/rvq_bench.py --batch 64 --nq 32 --variants 3 --paths pt,2
+has rvqb10 && run rvq_b1x10 180 python tools/rvq_bench.py --batch 1 --frames 862 --nq 8 --variants 3 --paths pt,2
 has stamps && TAIL=50 run stamps 120 python tools/rvq_fused_stamps.py --pt
-has stampsfm && TAIL=50 run stampsfm 120 python tools/rvq_fused_stamps.py --fm
+
 has bench && run bench 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
-has benchfm && run benchfm 300 env VRVQ_RVQ_PROJ=0 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
+has benchz && run benchz 300 env VRVQ_RVQ_PROJ=0 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
 has benchfull && run benchfull 500 python bench.py
 has cfg3 && run cfg3 300 python bench.py --batch 64 --n-codebooks 32 --steps 10 --warmup 2 --no-cpu-baseline
 has sweep && run sweep 300 python bench.py --sweep --steps 10 --warmup 2 --no-cpu-baseline

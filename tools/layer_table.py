@@ -41,14 +41,6 @@ def _fake():
                       False))
         return torch.empty(8, B * tout, 8 * nq), (torch.empty(B, cout, tout) if want_z else None)
 
-    def conv1d_fm(x, wp, cout, k, pad=0, dil=1, bias=None, alpha=None, inv_alpha=None,
-                  w_x3=None):
-        B, cin, tin = x.shape
-        tout = tin + 2 * pad - dil * (k - 1)
-        CALLS.append(("conv", cin, cout, k, 1, dil, tout, B, 2.0 * B * cout * tout * cin * k,
-                      False))
-        return torch.empty(B, tout, cout)
-
     def convt(x, wp, cout, cout_pad, stride, bias=None, alpha=None, inv_alpha=None,
               out_snake=None, want_raw=True, pad=-1, w_x3=None):
         B, cin, tin = x.shape
@@ -114,9 +106,7 @@ def _fake():
     ops.rvq_encode = rvq_encode
     ops.rvq_encode_part = rvq_encode_part
     ops.conv1d_proj = conv1d_proj
-    ops.conv1d_fm = conv1d_fm
     ops.rvq_pack_w_in = lambda w: w
-    ops.rvq_encode_fm = lambda zt, w3in, *a, **k: rvq_encode(zt.transpose(1, 2), None, *a, **k)
     ops.rvq_frag = lambda cbn: cbn
     ops.rvq_codes = rvq_codes
     ops.rvq_expand = rvq_expand

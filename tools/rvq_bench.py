@@ -31,11 +31,11 @@ def main():
     ap.add_argument("--frames", type=int, default=87)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-zqis", action="store_true", help="want_z_q_is=False (z_q only)")
-    ap.add_argument("--variants", default="3,2", help="projection kernel variants to time (1,2,3)")
-    ap.add_argument("--paths", default="pt,fm,2,1",
+    ap.add_argument("--variants", default="3,2", help="projection kernel variants to time (2,3)")
+    ap.add_argument("--paths", default="pt,2,1",
                     help="RVQ launch structures to time (pt: the launch from the conv's projection "
-                         "partials, the eval encode's; fm: frame-major fused launch, 2 fused, 1 "
-                         "three launches)")
+                         "partials, the eval encode's; on channel-major z: 2 fused, 1 three "
+                         "launches)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     model = vrvq_amd.DAC_VRVQ(n_codebooks=args.nq)
@@ -48,11 +48,6 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     run = lambda: ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0,  # noqa: E731
                                  want_z_q_is=not args.no_zqis)
-    zt = z.transpose(1, 2).contiguous()
-    w3in = st.w3in()
-    run_fm = lambda: ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,  # noqa: E731
-                                       st.b_out, st.mcol, st.qb, imp=imp, level=1.0,
-                                       want_z_q_is=not args.no_zqis)
     from vrvq_amd import _lib
     part = torch.empty(8, args.batch * args.frames, args.nq * 8, device=dev)
     import ctypes
@@ -64,14 +59,12 @@ def main():
                                          want_z_q_is=not args.no_zqis)
     runs = []
     for p in args.paths.split(","):
-        if p in ("fm", "pt"):
+        if p == "pt":
             runs.append((p, 0))
         else:
             runs += [(int(p), int(x)) for x in args.variants.split(",")]
     for path, v in runs:
-        if path == "fm":
-            run = run_fm
-        elif path == "pt":
+        if path == "pt":
             run = run_pt
             _lib.rvq_path(2)  # (a numeric path left at 1 would select pt's two-launch form)
         else:

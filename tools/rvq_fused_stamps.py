@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Timeline of the fused RVQ launch (rvq_fused_kernel) from in-kernel s_memrealtime stamps
+"""Timeline of a fused RVQ launch (rvq_fused_kernel, or rvq_pt_kernel with --pt) from in-kernel s_memrealtime stamps
 (100 MHz, one clock for the whole chip; diagnostic build vrvq_amd/libvrvq_hip_stamps.so, built
 with `python -m vrvq_amd.build --stamps`). Thread 0 of every workgroup records:
   projection / chain workgroups: 0 start | 44 z slab in LDS (x3 projection) | 45 projection
@@ -32,9 +32,6 @@ def main():
                     help="z_q_is not materialised (the expansion writes z_q only)")
     ap.add_argument("--no-expand-mfma", action="store_true",
                     help="timing experiment: the expansion skips its MFMAs (outputs not checked)")
-    ap.add_argument("--fm", action="store_true",
-                    help="the frame-major launch (vrvq_rvq_encode_fm: chain parts project their "
-                         "own frames)")
     ap.add_argument("--pt", action="store_true",
                     help="the launch from the conv's projection partials (vrvq_rvq_encode_part: "
                          "rvq_pt_kernel; partials made here by vrvq_rvq_project)")
@@ -70,9 +67,7 @@ def main():
     grid = 2 * B * 8
     stamps = torch.zeros(grid * 64, dtype=torch.int64, device=dev)
 
-    zt = z.transpose(1, 2).contiguous()
-    w3in = st.w3in()
-    assert T <= 128, "the frame-major timeline assumes 8 chain parts per clip"
+    assert args.pt or T <= 96, "rvq_fused_kernel: T <= 96"
 
     if args.pt:
         part = torch.empty(8, B * T, nq * 8, device=dev)
@@ -81,7 +76,7 @@ def main():
         assert lib.vrvq_rvq_workspace_part(B, T, nq, 1024, ctypes.byref(n2)) == 0
         wsp = torch.empty((n2.value + 3) // 4, device=dev)
         F_env = int(os.environ.get("VRVQ_RVQ_PT_F", "0"))
-        F = min(F_env, T) if 1 <= F_env <= 16 else ((T + 7) // 8 if T <= 128 else 16)
+        F = min(F_env, T) if 1 <= F_env <= 16 else min(16, T)  # pt_frames_per_part
         P_parts = (T + F - 1) // F
         n_fb = (T + 95) // 96
         grid = B * (P_parts + 8 * n_fb)
@@ -96,15 +91,6 @@ def main():
                                           P(codes), P(lat), P(loss),
                                           None if args.no_zqis else P(zqis), P(zq), P(mask),
                                           P(wsp), ctypes.c_longlong(wsp.numel() * 4), stream)
-            assert rc == 0, rc
-            return
-        if args.fm:
-            rc = lib.vrvq_rvq_encode_fm(P(zt), B, 1024, T, nq, 1024, 8, P(w3in), P(st.b_in),
-                                        P(st.cb), P(st.cbf), P(st.c2), P(st.w_out), P(st.b_out),
-                                        P(st.mcol), P(st.qb), P(imp), ctypes.c_float(1.0),
-                                        P(codes), P(lat), P(loss),
-                                        None if args.no_zqis else P(zqis), P(zq), P(mask), None,
-                                        ctypes.c_longlong(0), stream)
             assert rc == 0, rc
             return
         rc = lib.vrvq_rvq_encode(P(z), B, 1024, T, nq, 1024, 8, P(st.w_in_t), P(st.b_in),
@@ -132,9 +118,6 @@ def main():
     if args.pt:
         ref = vrvq_amd.ops.rvq_encode_part(part, T, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
                                            st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
-    elif args.fm:
-        ref = vrvq_amd.ops.rvq_encode_fm(zt, w3in, st.b_in, st.cb, st.cbf, st.c2, st.w_out,
-                                         st.b_out, st.mcol, st.qb, imp=imp, level=1.0)
     else:
         ref = vrvq_amd.ops.rvq_encode(z, *st.codes_args(), imp=imp, level=1.0)
     nocheck = os.environ.get("VRVQ_STAMPS_NOCHECK") == "1"  # timing-only experiment builds
@@ -158,11 +141,8 @@ def main():
     print("projection / chain workgroups")
     row("start", pc[:, 0])
     if not args.pt:
-        row("z slab in LDS" if not args.fm else "K-half 0 staged", pc[:, 44])
-        if args.fm:
-            row("K-half 1 staged", pc[:, 46])
+        row("z slab in LDS", pc[:, 44])
         row("projection MFMAs + stores issued", pc[:, 45])
-    if not args.fm and not args.pt:
         row("clip's partials seen (thread 0)", pc[:, 2])
     row("prologue done", pc[:, 3])
     for i in range(nq):

@@ -26,7 +26,6 @@ SIGNATURES = {
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
-    "vrvq_conv1d_fm": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "vrvq_conv1d_proj": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                          _P, _P],
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
@@ -45,9 +44,6 @@ SIGNATURES = {
                         _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_rvq_w_in_planes_size": [_I, _I, _I, _P],
     "vrvq_rvq_pack_w_in": [_P, _I, _I, _I, _P, _P],
-    "vrvq_rvq_workspace_fm": [_I, _I, _I, _I, _P],
-    "vrvq_rvq_encode_fm": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                           _F, _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_rvq_workspace_part": [_I, _I, _I, _I, _P],
     "vrvq_rvq_encode_part": [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
                              _P, _P, _P, _P, _P, _P, _P, ctypes.c_longlong, _P],

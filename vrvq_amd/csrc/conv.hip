@@ -824,30 +824,6 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
   return dispatch_ks(k, a, batch, as_stream(stream));
 }
 
-extern "C" int vrvq_conv1d_fm(const float* x, int batch, int cin, int tin, const float* alpha,
-                              const float* inv_alpha, const float* w_packed,
-                              const uint16_t* w_x3, int cout, int cout_pad, int k, int pad,
-                              int dil, const float* bias, float* y_fm, int tout,
-                              vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(x && w_packed && y_fm);
-  VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && dil > 0 && pad >= 0 &&
-                 tout > 0);
-  VRVQ_CHECK_ARG(cout_pad >= cout && cout_pad % 128 == 0 && cout % 4 == 0);
-  VRVQ_CHECK_ARG(alpha == nullptr || inv_alpha != nullptr);
-  VRVQ_CHECK_ARG(((uintptr_t)y_fm & 15) == 0);
-  const long long expect = (long long)tin + 2LL * pad - (long long)dil * (k - 1);
-  VRVQ_CHECK_ARG(expect == tout);
-  ConvArgs a{};
-  a.x = x; a.alpha = alpha; a.inv_alpha = inv_alpha; a.w = w_packed; a.bias = bias;
-  a.yfm = y_fm;
-  a.cin = cin; a.tin = tin; a.M = cout; a.m_pad = cout_pad; a.cout = cout;
-  a.stride = 1; a.pad = pad; a.dil = dil; a.ng = tout; a.up = 0; a.up_pad = 0; a.ssh = 0;
-  a.ylen = tout; a.epi = VRVQ_EPI_NONE;
-  a.w3 = reinterpret_cast<const unsigned*>(w_x3);
-  // the MFMA tiles only (their epilogue owns the frame-major store)
-  return dispatch_ks(k, a, batch, as_stream(stream));
-}
-
 extern "C" int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, const float* alpha,
                                 const float* inv_alpha, const float* w_packed,
                                 const uint16_t* w_x3, int cout, int cout_pad, int k, int pad,

@@ -37,9 +37,6 @@ struct ConvArgs {
   // phase-split view xv[c*s + r][m] = x[c][m*s + r - ppad] (conv_x3.h): cin / tin above are the
   // view's (pcin * s, tout + 1), x is [B][pcin][ptin]. psh = 0: no view.
   int psh, ppad, pcin, ptin;
-  // Frame-major output yfm[B][ng][M] (y of the encoder's last conv as the RVQ's zt,
-  // vrvq_conv1d_fm): written straight from the accumulators with the bias, instead of y.
-  float* yfm;
   // in_proj of every RVQ stage in the epilogue (vrvq_conv1d_proj, 128-row tiles of the
   // 1024-channel z): pj_part[s][b * ng + n][8 pj_nq] over the tile's channel split s = m0 / 128,
   // W_in as bf16 planes in the 16x16x32 A-fragment order (vrvq_rvq_pack_w_in); null: none
@@ -423,35 +420,8 @@ __device__ __forceinline__ void conv_epilogue(
   if constexpr (BM == 128) {
     if (a.pj_part) {
       proj_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
-      if (!a.yfm && !a.y && !a.ys) return;  // z itself not wanted: the partials are its use
+      if (!a.y && !a.ys) return;  // z itself not wanted: the partials are its use
     }
-  }
-  if (a.yfm) {
-    // frame-major: lane (col, lh) holds rows 8 q + 4 lh + (0..3) of column col for q = 0..3 --
-    // one 16-B store per (tile, q), the two lane halves' 16 B adjacent (32-B runs per column;
-    // a wave's four q stores fill each column's 128 B, merged in L2 before they leave it)
-    const int mrows = a.M - m0;
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int n = n0 + wn * TN + j * 32 + lr;
-        if (n >= a.ng) continue;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ml = wm * TM + i * 32 + 8 * q + 4 * lh;  // rows ml .. ml + 3 (M % 4 == 0)
-          if (ml >= mrows) continue;
-          const int m = m0 + ml;
-          float4 v = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
-                                 acc[i][j][4 * q + 3]);
-          if (a.bias) {
-            v.x = v.x + a.bias[m]; v.y = v.y + a.bias[m + 1];
-            v.z = v.z + a.bias[m + 2]; v.w = v.w + a.bias[m + 3];
-          }
-          *reinterpret_cast<float4*>(a.yfm + ((size_t)b * a.ng + n) * a.M + m) = v;
-        }
-      }
-    return;
   }
   // ---- epilogue through LDS (every stage buffer is free after the loop's last barrier) ----
   // The accumulator tile is transposed to row-major [BM][BNP] (EPASS column passes) so that

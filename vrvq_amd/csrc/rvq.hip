@@ -8,23 +8,23 @@
 // By linearity z_e(i) = ((P_i + b_in(i)) - Qb_i) - sum_{j<i} M_ij zst_j with P_i = W_in(i) z,
 // M_ij = W_in(i) W_out(j) (8x8) and Qb_i = W_in(i) sum_{j<i} b_out(j): the sequential part
 // lives in the 8-dim latent space and the 1024-dim work becomes two embarrassingly parallel
-// streams. The product path is ONE launch (rvq_fm_kernel: chain parts project their own frames
-// of the encoder's frame-major z, expansion workgroups write z_q_is / z_q; rvq_fused_kernel:
-// the same on channel-major z for T <= 96, with projection units); both are built from the
-// bodies of the three-launch form, which stays as the reference path:
+// streams. The eval encode's path is ONE launch from the in_proj partials the encoder's last
+// conv computes in its epilogue (rvq_pt_kernel: chain parts + expansion workgroups that write
+// z_q_is / z_q; conv.hip vrvq_conv1d_proj); on z itself, rvq_fused_kernel (projection units,
+// chain parts and expansion in one launch for T <= 96). Both are built from the bodies of the
+// three-launch form, which stays as the reference path:
 //
-//   rvq_project_kernel   P partials over 8 channel splits (v_mfma_f32_16x16x4_f32): each
-//                        workgroup streams a 48-frame tile of one clip's 128-channel slab of
-//                        z once (all loads issued up front, 4 K chunks in their own LDS
-//                        buffers consumed as they land; two workgroups per CU).
+//   rvq_project{3,2}_kernel  P partials over 8 channel splits (one workgroup per clip x 96-frame
+//                        tile x split, the z slab staged once in LDS; 3: split-bf16 MFMA, 2:
+//                        fp32-input v_mfma_f32_16x16x4_f32).
 //   rvq_chain_kernel     the chain: <= 16 frames per workgroup, 8 waves; wave w scans its
 //                        N/8 codes for all frames at once on the matrix cores (16-code x
 //                        16-frame MFMA tiles), then 8 (frame, k) lane groups finish the stage
 //                        (cross-wave argmin, raw codeword, loss, projected residual, next z_e)
 //                        — two barriers per stage, no global stores until the end.
 //   rvq_expand_kernel    z_q_is[b,i,:,:] = W_out(i) zst_i + b_out(i) and the masked sum z_q on
-//                        the matrix cores (32-channel x 32-frame tiles, bias as a 9th k): the
-//                        HBM write stream, with no LDS and a few VALU per element.
+//                        the matrix cores (32-channel x 32-frame tiles): the HBM write stream,
+//                        with no LDS and a few VALU per element.
 //
 // The distance is the reference's fp32 expression (dot in k order, fma(d, -2, e2) + c2, lowest
 // index on ties); the projection on the split-bf16 matrix cores (x3) is fp32-accurate but not
@@ -66,9 +66,8 @@ constexpr int RD = 1024;        // latent channels
 constexpr int RCD = 8;          // codebook_dim
 constexpr int PJ_SPLIT = 8;     // channel splits of the projection GEMM
 constexpr int PJ_CPS = RD / PJ_SPLIT;
-constexpr int PJ_TC = 48;       // frames per projection tile (3 MFMA column tiles)
-constexpr int PJ_ZLD = 48;      // z_s row stride (== 16 mod 32: conflict-free B reads)
-constexpr int PJ_WLD = 80;      // w_s row stride (== 16 mod 32: conflict-free A reads)
+constexpr int PJ_KC = 32;       // channels per projection K chunk
+constexpr int PJ_NC = PJ_CPS / PJ_KC;  // K chunks per split (4)
 constexpr int CH_NT = 512;      // chain threads (8 waves)
 constexpr int CH_NW = CH_NT / 64;
 constexpr int CH_FMAX = 16;     // frames per chain workgroup
@@ -157,113 +156,9 @@ __global__ void rvq_frag_kernel(const float* __restrict__ cbn, int nq, int N,
 
 // ------------------------------------------------------------------------------------------
 // Projection: part[s][n][r] = sum_{c in split s} W_in_t[r/8][c][r%8] z[b][c][t], n = b*T + t,
-// r < R = nq*8. Workgroup = (clip b, frame tile of <= 48, channel split s, 64-row block), 4
-// waves: wave w computes rows 16 w .. +15 for the 3 column tiles with v_mfma_f32_16x16x4_f32.
-// All of the workgroup's loads (the [128 ch][48 t] slab of z: row segments of one clip, and its
-// [128][64] weight block) are issued up front, in 4 K chunks of 32 channels, each chunk to its
-// own LDS buffer: chunk c is stored (waiting only for its own loads -- they complete in issue
-// order) and consumed by the MFMAs while chunks c+1.. are still landing. 64 KB of LDS: two
-// workgroups per CU, so one's loads overlap the other's MFMAs. Output: lane l holds 4
-// consecutive rows of one frame -> one float4 store.
-constexpr int PJ_NT = 256;
-constexpr int PJ_KC = 32;                       // channels per K chunk
-constexpr int PJ_NC = PJ_CPS / PJ_KC;           // chunks (4)
-constexpr int PJ_ZQ = PJ_KC * PJ_TC / PJ_NT;    // z loads per thread per chunk (6)
-constexpr int PJ_WQ = PJ_KC * 64 / 4 / PJ_NT;   // weight float4 per thread per chunk (2)
-constexpr int PJ_STG = PJ_KC * PJ_ZLD + PJ_KC * PJ_WLD;
-
-__global__ __launch_bounds__(PJ_NT) void rvq_project_kernel(const float* __restrict__ z, int T,
-                                                            int nq, int n_tc,
-                                                            const float* __restrict__ w_in_t,
-                                                            float* __restrict__ part, int NF) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // PJ_NC * PJ_STG floats
-  const int tc = blockIdx.x % n_tc, b = blockIdx.x / n_tc;
-  const int s = blockIdx.y, rb = blockIdx.z;
-  const int R = nq * RCD;
-  const int t0 = tc * PJ_TC;
-  const int ntl = min(PJ_TC, T - t0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float* zb = z + ((size_t)b * RD + s * PJ_CPS) * T + t0;
-  float zv[PJ_NC][PJ_ZQ];
-  float4 wv[PJ_NC][PJ_WQ];
-#pragma unroll
-  for (int kc = 0; kc < PJ_NC; ++kc) {  // every load of the workgroup in flight at once
-#pragma unroll
-    for (int q = 0; q < PJ_ZQ; ++q) {
-      const int e = tid + PJ_NT * q;
-      const int c = e / PJ_TC, t = e - c * PJ_TC;
-      // clamped address, zeroed at the LDS store (no branch: a guarded load becomes an
-      // exec-masked branch and the waitcnt pass then drains every outstanding load at the join)
-      zv[kc][q] = zb[(size_t)(kc * PJ_KC + c) * T + min(t, ntl - 1)];
-    }
-    // 8 stages x 32 channels x 2 float4
-#pragma unroll
-    for (int h = 0; h < PJ_WQ; ++h) {
-      const int e = tid + PJ_NT * h, sl = e >> 6, rem = e & 63;
-      const int st = rb * 8 + sl;
-      wv[kc][h] = ld4(w_in_t + ((size_t)min(st, nq - 1) * RD + s * PJ_CPS + kc * PJ_KC) * RCD +
-                      rem * 4);
-    }
-  }
-  const int lr = lane & 15, lk = lane >> 4;
-  f32x4 acc[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kc = 0; kc < PJ_NC; ++kc) {
-    float* z_s = sm + kc * PJ_STG;
-    float* w_s = z_s + PJ_KC * PJ_ZLD;
-#pragma unroll
-    for (int q = 0; q < PJ_ZQ; ++q) {
-      const int e = tid + PJ_NT * q;
-      const int c = e / PJ_TC, t = e - c * PJ_TC;
-      // bit mask, not a select: LLVM sinks a load whose only use is a select into a branch
-      z_s[c * PJ_ZLD + t] = __uint_as_float(__float_as_uint(zv[kc][q]) & (0u - (unsigned)(t < ntl)));
-    }
-#pragma unroll
-    for (int h = 0; h < PJ_WQ; ++h) {
-      const int e = tid + PJ_NT * h, sl = e >> 6, rem = e & 63;
-      const unsigned m = 0u - (unsigned)(rb * 8 + sl < nq);
-      const float4 w = wv[kc][h];
-      *reinterpret_cast<float4*>(w_s + (rem >> 1) * PJ_WLD + sl * 8 + (rem & 1) * 4) =
-          make_float4(__uint_as_float(__float_as_uint(w.x) & m), __uint_as_float(__float_as_uint(w.y) & m),
-                      __uint_as_float(__float_as_uint(w.z) & m), __uint_as_float(__float_as_uint(w.w) & m));
-    }
-    __syncthreads();
-    // all column tiles unconditionally (zero-padded frames): a runtime-guarded MFMA makes the
-    // compiler shuffle the accumulators through v_mov / accvgpr copies every step
-#pragma unroll
-    for (int kk = 0; kk < PJ_KC / 4; ++kk) {
-      const int c = kk * 4 + lk;
-      const float av = w_s[c * PJ_WLD + wave * 16 + lr];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const float bv = z_s[c * PJ_ZLD + j * 16 + lr];
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
-      }
-    }
-  }
-  const int r0 = rb * 64 + wave * 16;
-  // D layout: lane l, reg q -> row 4*(l>>4) + q of the wave's 16, column (frame) l & 15
-  const int rr = r0 + 4 * lk;  // R = 8 nq: rows rr..rr+3 are all valid iff rr < R
-  if (rr >= R) return;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int t = j * 16 + lr;
-    if (t < ntl) {
-      const size_t n = (size_t)b * T + t0 + t;
-      *reinterpret_cast<float4*>(part + ((size_t)s * NF + n) * R + rr) =
-          make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Projection, one workgroup per (clip, frame tile of <= 96, channel split): the same partials,
-// bit for bit, as rvq_project_kernel (each wave runs that kernel's MFMA sequence: the split's
-// 128 channels in order, 4 per v_mfma_f32_16x16x4_f32, from a zero accumulator), reorganised so
-// that a workgroup reads its z slab [128 ch][<= 96 t] from HBM once (row segments, staged in
+// r < R = nq*8, fp32-input form (variant 2). One workgroup per (clip, frame tile of <= 96,
+// channel split); each wave runs the split's 128 channels in order, 4 per
+// v_mfma_f32_16x16x4_f32, from a zero accumulator (an exact fmaf-chain order); a workgroup reads its z slab [128 ch][<= 96 t] from HBM once (row segments, staged in
 // LDS in four 32-channel chunks, each consumed as soon as it has landed) and keeps it for every
 // 64-row block of stages; the w_in_t operands go straight to registers (32 per lane and block).
 // 8 waves: wave w = 16-row tile (w & 3) x three 16-frame column tiles (w >> 2). 256 workgroups
@@ -672,10 +567,9 @@ struct ChainHandoff {              // fused launches only
 
 // Where a chain part gets pu = (P + b_in) - Qb of its frames: CH_SPLIT the 8 split partials of
 // the three-launch path (plain loads after the projection kernel), CH_GRANULE the tagged
-// partial granules of rvq_fused_kernel, CH_LOCAL already in LDS (rvq_fm_kernel's own projection),
-// CH_PART the 8 split partials the encoder's last conv wrote in its epilogue (vrvq_conv1d_proj;
+// partial granules of rvq_fused_kernel, CH_PART the 8 split partials the encoder's last conv wrote in its epilogue (vrvq_conv1d_proj;
 // plain loads after that kernel's boundary) in rvq_pt_kernel, which publishes every stage.
-constexpr int CH_SPLIT = 0, CH_GRANULE = 1, CH_LOCAL = 2, CH_PART = 3;
+constexpr int CH_SPLIT = 0, CH_GRANULE = 1, CH_PART = 3;
 
 template <int NM, int MODE>
 __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0, int nf,
@@ -729,9 +623,7 @@ __device__ __forceinline__ void chain_body(const ChainArgs& a, float* sm, int n0
   // ---- prologue: pu = (P + b_in) - Qb (partials summed in split order); stage 0 operands.
   __shared__ int dead_s;  // a bounded wait ran out in this workgroup: outputs poisoned
   if (tid == 0) dead_s = 0;
-  if constexpr (MODE == CH_LOCAL) {
-    // pu_s filled by the caller (project_fm_body) before the barrier that precedes this call
-  } else if constexpr (MODE == CH_GRANULE) {
+  if constexpr (MODE == CH_GRANULE) {
     // the clip's 8 partials of this part's frames: tagged granules (16-B sc1 loads, two each),
     // each thread re-reads its item until every tag is this call's (the projection units of
     // the clip run concurrently on other CUs); R = 8 nq: the frames' rows are contiguous
@@ -1160,11 +1052,10 @@ __global__ __launch_bounds__(256) void rvq_expand_kernel(ExpandArgs a) {
 // of clip b (frames [s F, s F + F), F = ceil(T / 8)), which reads the clip's 8 partials of its
 // frames as they land and publishes every stage's zst.
 //
-// rvq_fm_kernel (frame-major zt [B][T][D], any T): workgroups [0, B P) are chain parts (clip b,
-// frames [p F, p F + F), F <= 16) that project their own frames (project_fm_body: the part's zt
-// rows are contiguous, no partial leaves the workgroup) and run the chain.
+// rvq_pt_kernel (below: from the encoder conv's projection partials, any T): workgroups
+// [0, B P) are chain parts (clip b, frames [p F, p F + F), F <= 16).
 //
-// In both, the workgroups after the chain parts are the expansion: (clip b, 128-frame block fb,
+// In both, the workgroups after the chain parts are the expansion: (clip b, frame block fb,
 // 128-channel block cb) over all stages, each stage once the chain parts of its frames have
 // published it, so the z_q_is write stream runs under the chain instead of after it. Same
 // expressions as the three launches (tests/test_gpu_parity.py).
@@ -1178,9 +1069,8 @@ constexpr int FU_CLIPS_MAX = 32;    // clips per rvq_fused_kernel launch
 
 struct FusedArgs {
   ChainArgs c;                      // part (workspace), B, T, nq, F, NF; outputs
-  const float* z;                   // [B][D][T] (rvq_fused_kernel) or zt [B][T][D] (rvq_fm_kernel)
+  const float* z;                   // [B][D][T] (rvq_fused_kernel)
   const float* w_in_t;
-  const u32x4* w3in;                // rvq_fm_kernel: W_in planes (vrvq_rvq_pack_w_in)
   const float* w_out;               // [nq][D][8]
   const float* b_out;               // [nq][D]
   float* z_q_is;                    // [B][nq][D][T] or null
@@ -1199,8 +1089,6 @@ struct FusedArgs {
                                     // bit 1 = chain parts skip the next stage's codebook
                                     // fragment loads (outputs wrong; timing only)
   int warm;                         // expansion workgroups pull the stage tables into L2 first
-  int xf;                           // rvq_pt_kernel expansion knobs (VRVQ_RVQ_XF, A/B): bit 0
-                                    // s_setprio(1) on the compute waves, bit 1 probe polls
 };
 
 // The stage tables the chain and the expansion read after stage 0 (normalised / raw codebooks,
@@ -1509,223 +1397,9 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_fused_kernel(FusedArgs f) {
   chain_body<NM, CH_GRANULE>(f.c, sm, b * T + s * F, nf, hx);
 }
 
-// ------------------------------------------------------------------------------------------
-// Local projection of one chain part of rvq_fm_kernel: pu[f][r] = (P[f][r] + b_in[r]) - qb[r],
-// P[f][r] = sum_c W_in[r][c] zt[b][t0 + f][c], for the part's nf <= 16 frames and every row
-// r < R = 8 nq, on v_mfma_f32_16x16x32_bf16 with both operands split exactly into three bf16
-// terms and the six products of conv_x3.h (dropped terms <= 2^-23 |ab|: fp32 accuracy). The
-// part's zt rows are contiguous (4 KB each: no line amplification), staged in LDS as three bf16
-// planes one K-half (512 channels) at a time, [plane][frame][channel] with 1040-B rows
-// (conflict-free 16-B B-operand reads); W_in comes pre-split in the MFMA A-fragment order
-// (w3in [32 k-steps][3 planes][R/16 row tiles][64 lanes] x 16 B, vrvq_rvq_pack_w_in), read
-// from L2 straight into registers, four k-steps in flight. Work item = (row tile rt, K part kq)
-// with S K parts when fewer than 8 row tiles (nq = 8: 4 tiles x 2 parts over the 8 waves); the
-// S partial accumulators are summed in kq order through LDS. Frames >= nf are clamped copies
-// whose output columns are never read.
-constexpr int LP_LD = 520;                        // bf16 per frame row of a K-half plane
-constexpr int LP_PLANE = FU_ROWS * LP_LD * 2;     // bytes per plane (16 frame rows)
-constexpr int LP_LDS = 3 * LP_PLANE;              // 49,920 B
-
-__host__ __device__ inline int fm_nrt(int nq) { return (nq * RCD + 15) / 16; }
-__host__ __device__ inline int fm_ksplit(int nq) {  // K parts per row tile
-  const int n = fm_nrt(nq);
-  return n >= 8 ? 1 : n >= 4 ? 2 : n >= 2 ? 4 : 8;
-}
-// LDS of rvq_fm_kernel: the chain carve, overlaid by the K-half planes during the projection,
-// then the S - 1 partial tiles of the K split
-static_assert(LP_LDS >= FU_EX_LDS, "the expansion's zst slab fits the projection's LDS");
-__host__ __device__ inline size_t fm_lds_bytes(int nq, int F, int N) {
-  size_t c = (size_t)ChainLds(nq, F, N).total * sizeof(float);
-  if (c < (size_t)LP_LDS) c = LP_LDS;
-  const int S = fm_ksplit(nq);
-  return c + (size_t)(S - 1) * fm_nrt(nq) * 64 * 16;
-}
-
-// NKS consecutive k-steps (32 channels each) of one 16-row tile against the staged K-half:
-// the A planes come from L2 in a ring three k-steps deep (36 VGPRs in flight per lane), each
-// k-step's six products in the x3 order m m, h l, l h, h m, m h, h h.
-#ifdef VRVQ_PJ_ROT
-// timing experiment only (another k order per workgroup: not bit-identical across positions)
-#define FM_ROT(j) (((j) + (int)blockIdx.x) % NKS)
-#else
-#define FM_ROT(j) (j)
-#endif
-#ifdef VRVQ_PJ_2PL
-#define FM_PL(p) ((p) == 2 ? -1 : (p))  // timing experiment only: two of the three W planes
-#else
-#define FM_PL(p) (p)
-#endif
-constexpr int FM_DEPTH = 4, FM_PRIME = 1;  // ring depth; k-steps primed under the z loads
-template <int NKS>
-__device__ __forceinline__ void fm_prime(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
-                                         u32x4 (&a)[FM_DEPTH][3], int j0 = 0,
-                                         int j1 = FM_PRIME) {
-  constexpr int DEPTH = NKS < FM_DEPTH ? NKS : FM_DEPTH;
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < DEPTH; ++j)
-    if (j >= j0 && j < j1)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) a[j][p] = FM_PL(p) < 0 ? a[j][0] : w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
-}
-// (primed: the ring's first DEPTH k-steps are already in flight in `a`, fm_prime)
-template <int NKS>
-__device__ __forceinline__ void fm_ksteps(const u32x4* __restrict__ w3, int n_rt, int rt, int ks0,
-                                          int h, const char* lds, f32x4& acc,
-                                          u32x4 (&a)[FM_DEPTH][3], bool primed) {
-  constexpr int DEPTH = NKS < FM_DEPTH ? NKS : FM_DEPTH;
-  const int lane = threadIdx.x & 63, lr = lane & 15, kg = lane >> 4;
-  auto load_a = [&](int j, u32x4 (&dst)[3]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) dst[p] = FM_PL(p) < 0 ? dst[0] : w3[((size_t)((ks0 + FM_ROT(j)) * 3 + p) * n_rt + rt) * 64 + lane];
-  };
-  fm_prime<NKS>(w3, n_rt, rt, ks0, a, primed ? FM_PRIME : 0, FM_DEPTH);
-#pragma unroll
-  for (int j = 0; j < NKS; ++j) {
-    const int kk = (ks0 + FM_ROT(j) - 16 * h) * 32 + 8 * kg;  // channel within the half
-    const char* bp = lds + lr * (LP_LD * 2) + kk * 2;
-    const u32x4 bh = *reinterpret_cast<const u32x4*>(bp);
-    const u32x4 bm = *reinterpret_cast<const u32x4*>(bp + LP_PLANE);
-    const u32x4 bl = *reinterpret_cast<const u32x4*>(bp + 2 * LP_PLANE);
-    const u32x4(&aj)[3] = a[j % DEPTH];
-    acc = mfma16_bf16(aj[1], bm, acc);  // m m
-    acc = mfma16_bf16(aj[0], bl, acc);  // h l
-    acc = mfma16_bf16(aj[2], bh, acc);  // l h
-    acc = mfma16_bf16(aj[0], bm, acc);  // h m
-    acc = mfma16_bf16(aj[1], bh, acc);  // m h
-    acc = mfma16_bf16(aj[0], bh, acc);  // h h
-    if (j + DEPTH < NKS) load_a(j + DEPTH, a[j % DEPTH]);  // compile-time condition
-  }
-}
-
-__device__ __forceinline__ void project_fm_body(const FusedArgs& f, int b, int t0, int nf,
-                                                int N, float* sm) {
-  const int nq = f.c.nq, R = nq * RCD, T = f.c.T;
-  const int n_rt = fm_nrt(nq), S = fm_ksplit(nq);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* lds = reinterpret_cast<char*>(sm);
-  const ChainLds L(nq, f.c.F, 256);  // only .pu is used here (independent of N)
-  float* pu_s = sm + L.pu;
-  const size_t c_bytes = [&] {  // fm_lds_bytes' carve: the partial tiles after the chain's LDS
-    size_t c = (size_t)ChainLds(nq, f.c.F, N).total * sizeof(float);
-    return c < (size_t)LP_LDS ? (size_t)LP_LDS : c;
-  }();
-  f32x4* xpart = reinterpret_cast<f32x4*>(lds + c_bytes);  // [S - 1][n_rt][64 lanes]
-  // the part's zt rows: thread (c4 = tid & 127, frame group tid >> 7) holds 4 float4 per K-half
-  // (frames (tid >> 7) + 4 u, channels 512 h + 4 c4 .. +3), all in flight at once
-  const float* zb = f.z + ((size_t)b * T + t0) * RD;
-  const int c4 = tid & 127, fg = tid >> 7;
-  float4 zv[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      zv[h][u] = ld4(zb + (size_t)min(fg + 4 * u, nf - 1) * RD + 512 * h + 4 * c4);
-  const u32x4* w3 = f.w3in;
-  const int n_items = n_rt * S;  // <= 16: at most two rounds of 8 items (S = 1 at nq > 14)
-  // items of this wave: it = wave, wave + 8 (rt = it / S, kq = it % S); the summed tiles stay in
-  // registers until every wave is done with the planes (pu_s shares their LDS)
-  f32x4 res[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int round = 0; round < 2; ++round) {
-    const int it0 = round * CH_NW;
-    if (it0 >= n_items) break;
-    const int it = it0 + wave;
-    const bool act = it < n_items;  // wave-uniform
-    const int rt = min(it, n_items - 1) / S, kq = min(it, n_items - 1) % S;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    // half 0's first k-steps of W_in in flight under the z loads and the slab's staging
-    u32x4 ring[FM_DEPTH][3];
-    {
-      const int ks0 = kq * (16 / S);
-      switch (S) {
-        case 1: fm_prime<16>(w3, n_rt, rt, ks0, ring); break;
-        case 2: fm_prime<8>(w3, n_rt, rt, ks0, ring); break;
-        case 4: fm_prime<4>(w3, n_rt, rt, ks0, ring); break;
-        default: fm_prime<2>(w3, n_rt, rt, ks0, ring); break;
-      }
-    }
-    for (int h = 0; h < 2; ++h) {
-      // stage K-half h (every item round: nq >= 16 runs more than one round)
-      __syncthreads();  // the previous half's planes are no longer read
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        // select, not zv[h][u]: a runtime index sends the array to scratch
-        const float4 v = h ? zv[1][u] : zv[0][u];
-        unsigned hh[2], mm[2], ll[2];
-        rvq_split3x2(v.x, v.y, hh[0], mm[0], ll[0]);
-        rvq_split3x2(v.z, v.w, hh[1], mm[1], ll[1]);
-        char* d = lds + (fg + 4 * u) * (LP_LD * 2) + c4 * 8;
-        *reinterpret_cast<uint2*>(d) = make_uint2(hh[0], hh[1]);
-        *reinterpret_cast<uint2*>(d + LP_PLANE) = make_uint2(mm[0], mm[1]);
-        *reinterpret_cast<uint2*>(d + 2 * LP_PLANE) = make_uint2(ll[0], ll[1]);
-      }
-      __syncthreads();
-      if (round == 0) FSTAMP(f.stamps, h == 0 ? 44 : 46);  // K-half h staged
-      if (act) {
-        // this item's k-steps of half h: ks = 16 h + kq * NKS + j, j < NKS = 16 / S
-        const int ks0 = 16 * h + kq * (16 / S);
-        const bool primed = h == 0;
-        switch (S) {
-          case 1: fm_ksteps<16>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
-          case 2: fm_ksteps<8>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
-          case 4: fm_ksteps<4>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
-          default: fm_ksteps<2>(w3, n_rt, rt, ks0, h, lds, acc, ring, primed); break;
-        }
-      }
-    }
-    // D layout: lane l, reg q -> row 16 rt + 4 (l >> 4) + q, frame l & 15
-    if (S > 1) {
-      if (act && kq > 0) xpart[((kq - 1) * n_rt + rt) * 64 + lane] = acc;
-      __syncthreads();
-    }
-    if (act && kq == 0) {
-      for (int q = 1; q < S; ++q) acc = acc + xpart[((q - 1) * n_rt + rt) * 64 + lane];
-      res[round] = acc;
-    }
-    if (S > 1) __syncthreads();  // xpart free for the next round
-  }
-  __syncthreads();  // every wave is done with the planes: pu_s may overwrite them
-#pragma unroll
-  for (int round = 0; round < 2; ++round) {
-    const int it = round * CH_NW + wave;
-    if (it >= n_items || it % S != 0) continue;
-    const int rt = it / S;
-    const int fr = lane & 15, rr = rt * 16 + 4 * (lane >> 4);
-    if (fr < nf && rr < R) {
-      const f32x4 acc = res[round];
-      float4 o;
-      o.x = (acc[0] + f.c.b_in[rr]) - f.c.qb[rr];
-      o.y = (acc[1] + f.c.b_in[rr + 1]) - f.c.qb[rr + 1];
-      o.z = (acc[2] + f.c.b_in[rr + 2]) - f.c.qb[rr + 2];
-      o.w = (acc[3] + f.c.b_in[rr + 3]) - f.c.qb[rr + 3];
-      *reinterpret_cast<float4*>(pu_s + fr * R + rr) = o;
-    }
-  }
-  __syncthreads();  // pu_s complete; the planes' LDS is the chain's from here
-}
-
-template <int NM>
-__global__ __launch_bounds__(CH_NT, 4) void rvq_fm_kernel(FusedArgs f) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int B = f.c.B, T = f.c.T, F = f.c.F;
-  const int blk = blockIdx.x;
-  FSTAMP(f.stamps, 0);
-  if (blk >= B * f.P) {
-    if (f.warm) warm_tables(f, blk - B * f.P, (int)gridDim.x - B * f.P, 256 * NM, sm);
-    fused_expand_body(f, blk - B * f.P, sm);
-    FSTAMP(f.stamps, 41);
-    return;
-  }
-  const int b = blk / f.P, p = blk - b * f.P;
-  const int t0 = p * F, nf = min(F, T - t0);
-  if (f.stall && blk == 0)  // test knob (vrvq_rvq_debug_stall): a late producer
-    for (unsigned k = 0; k < f.stall; ++k) __builtin_amdgcn_s_sleep(127);
-  project_fm_body(f, b, t0, nf, 256 * NM, sm);
-  FSTAMP(f.stamps, 45);
-  chain_body<NM, CH_LOCAL>(f.c, sm, b * T + t0, nf, fused_handoff(f, b, p));
-}
+// W_in planes of vrvq_conv1d_proj's projection epilogue (conv_core.h proj_epilogue): 16-row
+// tiles of the R = 8 nq stage rows
+__host__ __device__ inline int pj_nrt(int nq) { return (nq * RCD + 15) / 16; }
 
 // ------------------------------------------------------------------------------------------
 // rvq_pt_kernel: the quantizer from the projection partials that the encoder's last conv wrote
@@ -1983,15 +1657,8 @@ template <int NM>
 __global__ __launch_bounds__(CH_NT, 4) void rvq_pt_kernel(FusedArgs f) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int B = f.c.B, T = f.c.T, F = f.c.F;
-  int blk = blockIdx.x;
+  const int blk = blockIdx.x;
   FSTAMP(f.stamps, 0);
-  if ((f.xf & 4) && gridDim.x == 512 && B * f.P == 256) {
-    // A/B (VRVQ_RVQ_XF bit 2): roles by the observed dispatch order (block b -> XCD b % 8, that
-    // XCD's CU (b / 8) % 32, slot b / 256; speed only, any placement is correct): chain parts on
-    // CUs 0-15 of every XCD (two per CU), expansion on CUs 16-31
-    const int sl = blk >> 8, cu = (blk >> 3) & 31, x = blk & 7;
-    blk = cu < 16 ? sl * 128 + cu * 8 + x : 256 + sl * 128 + (cu - 16) * 8 + x;
-  }
   if (blk >= B * f.P) {
     pt_expand_body(f, blk - B * f.P, 256 * NM, sm);
     FSTAMP(f.stamps, 41);
@@ -2005,15 +1672,14 @@ __global__ __launch_bounds__(CH_NT, 4) void rvq_pt_kernel(FusedArgs f) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Projection kernel: 2 = rvq_project2_kernel (one workgroup per clip x split, default), 1 =
-// rvq_project_kernel (48-frame tiles x 64-row blocks). Same partials bit for bit (A/B timing and
-// the bit-identity test; VRVQ_RVQ_PROJECT=1 in the environment).
+// Projection kernel: 3 = rvq_project3_kernel (split-bf16 matrix cores, default), 2 =
+// rvq_project2_kernel (fp32-input MFMA: the exactness fallback, VRVQ_RVQ_PROJECT=2).
 int g_project_variant = 0;  // 0: not yet read from the environment
 
 int project_variant() {
   if (g_project_variant == 0) {
     const char* e = getenv("VRVQ_RVQ_PROJECT");
-    g_project_variant = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 3;
+    g_project_variant = (e && e[0] == '2') ? 2 : 3;
   }
   return g_project_variant;
 }
@@ -2022,33 +1688,18 @@ int launch_project(const float* z, int batch, int frames, int nq, const float* w
                    float* part, hipStream_t st) {
   const long long nf = (long long)batch * frames;
   VRVQ_CHECK_ARG(nf * nq * RCD * PJ_SPLIT < 0x7fffffffLL);
+  const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
+  VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
   if (project_variant() == 3) {
-    const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
-    VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
     hipError_t e = hipFuncSetAttribute((const void*)rvq_project3_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, PJ3_LDS);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(rvq_project3_kernel, dim3((unsigned)(batch * n_tc), PJ_SPLIT), dim3(PJ2_NT),
                        PJ3_LDS, st, z, frames, nq, n_tc, w_in_t, part, (int)nf);
-    return vrvq_launch_status();
-  }
-  if (project_variant() == 2) {
-    const int n_tc = (frames + PJ2_TC - 1) / PJ2_TC;
-    VRVQ_CHECK_ARG((long long)batch * n_tc < 0x7fffffffLL);
+  } else {
     hipLaunchKernelGGL(rvq_project2_kernel, dim3((unsigned)(batch * n_tc), PJ_SPLIT), dim3(PJ2_NT),
                        0, st, z, frames, nq, n_tc, w_in_t, part, (int)nf);
-    return vrvq_launch_status();
   }
-  const int n_tc = (frames + PJ_TC - 1) / PJ_TC;
-  const dim3 grid((unsigned)(batch * n_tc), PJ_SPLIT, (unsigned)((nq + 7) / 8));
-  const int lds = PJ_NC * PJ_STG * (int)sizeof(float);
-  if (lds > 64 * 1024) {  // the attribute is per device: set on every launch that needs it
-    hipError_t e = hipFuncSetAttribute((const void*)rvq_project_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return (int)e;
-  }
-  hipLaunchKernelGGL(rvq_project_kernel, grid, dim3(PJ_NT), lds, st, z, frames, nq, n_tc, w_in_t,
-                     part, (int)nf);
   return vrvq_launch_status();
 }
 
@@ -2370,55 +2021,8 @@ int launch_fused_nm(const FusedArgs& f0, int batch, int frames, int nq, const fl
   return 0;
 }
 
-// Frames per chain part of rvq_fm_kernel: T <= 128 (one expansion frame block per clip): 8
-// parts of ceil(T / 8); longer clips: 16 frames -- or fewer wherever the chain's LDS would not
-// fit twice per CU (beside an expansion workgroup): nq = 32 at T > 88.
-int fm_frames_per_part(int frames, int nq, int N) {
-  const int F0 = frames <= FU_FB ? (frames + 7) / 8 : FU_ROWS;
-  for (int F = F0; F >= 1; --F)
-    if (fm_lds_bytes(nq, F, N) <= 80 * 1024) return F;
-  return 0;
-}
-
-template <int NM>
-int launch_fm_nm(const FusedArgs& f0, int batch, int frames, int nq, const float* zt,
-                 const float* imp, int64_t* codes, float* latents, float* loss_pf,
-                 float* z_q_is, float* z_q, float* mask, void* ws, size_t ws_bytes,
-                 hipStream_t st) {
-  const int F = fm_frames_per_part(frames, nq, 256 * NM);
-  if (F < 1) return VRVQ_ERR_UNSUPPORTED;
-  const int P = (frames + F - 1) / F;
-  const int n_fb = (frames + FU_FB - 1) / FU_FB;
-  const size_t lds = fm_lds_bytes(nq, F, 256 * NM);
-  if (lds > 80 * 1024) return VRVQ_ERR_UNSUPPORTED;
-  const void* kern = (const void*)rvq_fm_kernel<NM>;
-  const int wpc = P + (RD / FU_CB) * n_fb;  // workgroups per clip
-  const int cap = fused_clip_capacity(kern, lds, wpc);
-  if (cap < 1) return VRVQ_ERR_UNSUPPORTED;
-  int bc_max = min(batch, cap);
-  while (bc_max > 1 && zsh_bytes(bc_max, nq, P) > 0x7fffffffULL) --bc_max;
-  const size_t need = zsh_bytes(bc_max, nq, P);
-  for (int b0 = 0; b0 < batch; b0 += bc_max) {
-    const int bc = min(bc_max, batch - b0);
-    FusedArgs f = f0;
-    FusedLaunch L;
-    if (!fused_prepare(st, need, ws, ws_bytes, &L)) return VRVQ_ERR_UNSUPPORTED;
-    fused_chunk_args(f, b0, bc, frames, nq, F, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask);
-    f.sync = L.sync;
-    f.epoch = L.epoch;
-    f.c.part = nullptr;
-    f.zsh = reinterpret_cast<unsigned long long*>(L.area);
-    f.zsh_bytes = (int)zsh_bytes(bc, nq, P);
-    f.P = P;
-    f.n_fb = n_fb;
-    const int rc = launch_timed(rvq_fm_kernel<NM>, (unsigned)(bc * wpc), lds, st, f);
-    if (rc) return rc;
-  }
-  return 0;
-}
-
-// Frames per chain part of rvq_pt_kernel: as rvq_fm_kernel (8 parts up to T = 128, else 16
-// frames), fewer wherever the chain's LDS would not fit twice per CU.
+// Frames per chain part of rvq_pt_kernel: 16, fewer wherever the chain's LDS would not fit twice
+// per CU (beside an expansion workgroup).
 size_t pt_lds_bytes(int nq, int F, int N) {
   size_t c = (size_t)ChainLds(nq, F, N).total * sizeof(float);
   const size_t ex = (size_t)PT_EX_FLOATS * sizeof(float);  // slab, warm-up sink, one z_q tile
@@ -2507,10 +2111,10 @@ int launch_pt_nm(const FusedArgs& f0, int batch, int frames, int nq, const float
   return 0;
 }
 
-// W_in planes of rvq_fm_kernel in the 16x16x32 A-fragment order: w3in[ks][plane][rt][lane] =
+// W_in planes of the conv projection epilogue in the 16x16x32 A-fragment order: w3in[ks][plane][rt][lane] =
 // 8 bf16 of row r = 16 rt + (lane & 15), channels 32 ks + 8 (lane >> 4) .. +7 (zero rows >= R).
 __global__ void rvq_pack_w_in_kernel(const float* __restrict__ w_in_t, int nq, u32x4* __restrict__ w3) {
-  const int n_rt = fm_nrt(nq), R = nq * RCD;
+  const int n_rt = pj_nrt(nq), R = nq * RCD;
   const int total = 32 * 3 * n_rt * 64;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
     const int lane = o & 63;
@@ -2552,7 +2156,7 @@ extern "C" int vrvq_debug_set_fused_flags(int flags) {
 
 extern "C" int vrvq_rvq_project_variant(int variant) {
   const int prev = project_variant();
-  if (variant >= 1 && variant <= 3) g_project_variant = variant;
+  if (variant == 2 || variant == 3) g_project_variant = variant;
   else if (variant != 0) return VRVQ_ERR_ARG;
   return prev;
 }
@@ -2765,7 +2369,7 @@ extern "C" int vrvq_rvq_encode(const float* z, int batch, int dim, int frames, i
 extern "C" int vrvq_rvq_w_in_planes_size(int nq, int dim, int cdim, long long* n_u16) {
   VRVQ_CHECK_ARG(n_u16 && nq > 0);
   if (dim != RD || cdim != RCD || nq > CH_NQMAX) return VRVQ_ERR_UNSUPPORTED;
-  *n_u16 = 32LL * 3 * fm_nrt(nq) * 64 * 8;
+  *n_u16 = 32LL * 3 * pj_nrt(nq) * 64 * 8;
   return 0;
 }
 
@@ -2773,55 +2377,10 @@ extern "C" int vrvq_rvq_pack_w_in(const float* w_in_t, int nq, int dim, int cdim
                                   vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(w_in_t && w3in && nq > 0);
   if (dim != RD || cdim != RCD || nq > CH_NQMAX) return VRVQ_ERR_UNSUPPORTED;
-  const int total = 32 * 3 * fm_nrt(nq) * 64;
+  const int total = 32 * 3 * pj_nrt(nq) * 64;
   hipLaunchKernelGGL(rvq_pack_w_in_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      as_stream(stream), w_in_t, nq, reinterpret_cast<u32x4*>(w3in));
   return vrvq_launch_status();
-}
-
-extern "C" int vrvq_rvq_workspace_fm(int batch, int frames, int nq, int ncode, long long* bytes) {
-  VRVQ_CHECK_ARG(bytes && batch > 0 && frames > 0 && nq > 0 && ncode > 0);
-  const int F = fm_frames_per_part(frames, nq, ncode);
-  if (F < 1) return VRVQ_ERR_UNSUPPORTED;
-  const int P = (frames + F - 1) / F;
-  *bytes = (long long)zsh_bytes(batch, nq, P) + (long long)FU_SYNC_BYTES;
-  return 0;
-}
-
-extern "C" int vrvq_rvq_encode_fm(const float* zt, int batch, int dim, int frames, int nq,
-                                  int ncode, int cdim, const uint16_t* w3in, const float* b_in,
-                                  const float* cb, const float* cbf, const float* c2,
-                                  const float* w_out, const float* b_out, const float* mcol,
-                                  const float* qb, const float* imp, float level, int64_t* codes,
-                                  float* latents, float* loss_pf, float* z_q_is, float* z_q,
-                                  float* mask, void* workspace, long long workspace_bytes,
-                                  vrvq_stream_t stream) {
-  VRVQ_CHECK_ARG(zt && w3in && b_in && cb && cbf && c2 && w_out && b_out && mcol && qb &&
-                 codes && latents && loss_pf && z_q);
-  VRVQ_CHECK_ARG(batch > 0 && frames > 0 && nq > 0 && workspace_bytes >= 0);
-  VRVQ_CHECK_ARG(((uintptr_t)workspace & 15) == 0);
-  if (!rvq_shape_ok(dim, cdim, nq, ncode)) return VRVQ_ERR_UNSUPPORTED;
-  FusedArgs f{};
-  ChainArgs& c = f.c;
-  c.b_in = b_in; c.qb = qb; c.mcol = mcol; c.cb = cb; c.cbf = cbf; c.c2 = c2;
-  c.level = level;
-  f.w3in = reinterpret_cast<const u32x4*>(w3in);
-  f.w_out = w_out;
-  f.b_out = b_out;
-  // VRVQ_RVQ_WARM=0: the expansion workgroups do not pull the stage tables into L2 (A/B)
-  static const int warm = [] {
-    const char* e = getenv("VRVQ_RVQ_WARM");
-    return e ? atoi(e) : 1;
-  }();
-  f.warm = warm;
-  hipStream_t st = as_stream(stream);
-  const size_t wsb = (size_t)workspace_bytes;
-  switch (ncode / 256) {
-    case 1: return launch_fm_nm<1>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
-    case 2: return launch_fm_nm<2>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
-    case 3: return launch_fm_nm<3>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
-    default: return launch_fm_nm<4>(f, batch, frames, nq, zt, imp, codes, latents, loss_pf, z_q_is, z_q, mask, workspace, wsb, st);
-  }
 }
 
 extern "C" int vrvq_rvq_workspace_part(int batch, int frames, int nq, int ncode, long long* bytes) {
@@ -2868,11 +2427,6 @@ extern "C" int vrvq_rvq_encode_part(const float* part, int batch, int dim, int f
     return e ? atoi(e) : 0;
   }();
   f.warm = warm;
-  static const int xf = [] {  // VRVQ_RVQ_XF: the expansion's A/B knobs (FusedArgs::xf)
-    const char* e = getenv("VRVQ_RVQ_XF");
-    return e ? atoi(e) : 0;
-  }();
-  f.xf = xf;
   hipStream_t st = as_stream(stream);
   const size_t wsb = (size_t)workspace_bytes;
   switch (ncode / 256) {

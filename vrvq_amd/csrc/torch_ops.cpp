@@ -223,35 +223,6 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
   return {y, ys};
 }
 
-// Snake1d -> WNConv1d with a FRAME-MAJOR output (B, T, Cout) (include/vrvq.h vrvq_conv1d_fm):
-// the encoder's last conv (models/dac_vrvq.py:34) writing z in rvq_encode_fm's zt layout.
-Tensor snake_conv1d_fm(const Tensor& x, const Tensor& w_packed, int64_t cout, int64_t pad,
-                       int64_t dil, const optional<Tensor>& bias, const optional<Tensor>& alpha,
-                       const optional<Tensor>& inv_alpha, const optional<Tensor>& w_x3) {
-  check_t(x, "x");
-  check_on(w_packed, x, "w_packed");
-  check_opt(bias, x, "bias");
-  check_opt(alpha, x, "alpha");
-  check_opt(inv_alpha, x, "inv_alpha");
-  TORCH_CHECK(x.dim() == 3, "conv1d_fm: x must be (B, C, T)");
-  TORCH_CHECK(w_packed.dim() == 3 && w_packed.size(0) == x.size(1),
-              "conv1d_fm: w_packed must be (Cin, k, cout_pad) with Cin = x.shape[1]");
-  TORCH_CHECK(alpha.has_value() == inv_alpha.has_value(), "conv1d_fm: snake needs inv_alpha");
-  c10::DeviceGuard guard(x.device());
-  const int64_t B = x.size(0), cin = x.size(1), tin = x.size(2);
-  const int64_t k = w_packed.size(1), cout_pad = w_packed.size(2);
-  const int64_t tout = tin + 2 * pad - dil * (k - 1);
-  TORCH_CHECK(tout > 0, "conv1d_fm: input too short");
-  Tensor y = empty_f({B, tout, cout}, x);
-  check_rc(vrvq_conv1d_fm(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                          fp(inv_alpha), w_packed.data_ptr<float>(),
-                          x3_ptr(w_x3, x, cin, k, cout_pad), (int)cout, (int)cout_pad, (int)k,
-                          (int)pad, (int)dil, fp(bias), y.data_ptr<float>(), (int)tout,
-                          stream_of(x)),
-           "vrvq_conv1d_fm");
-  return y;
-}
-
 // Snake1d -> WNConvTranspose1d (k = 2s) of DecoderBlock, models/layers.py:21-22, 92-103.
 std::tuple<Tensor, Tensor> snake_conv_transpose1d(
     const Tensor& x, const Tensor& w_packed, int64_t cout, int64_t stride,
@@ -426,7 +397,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode(
   return {codes, latents, loss_pf, z_q_is, z_q, mask};
 }
 
-// W_in planes for rvq_encode_fm (include/vrvq.h vrvq_rvq_pack_w_in), once per weight version.
+// W_in planes for snake_conv1d_proj (include/vrvq.h vrvq_rvq_pack_w_in), once per weight version.
 Tensor rvq_pack_w_in(const Tensor& w_in_t) {
   check_t(w_in_t, "w_in_t");
   TORCH_CHECK(w_in_t.dim() == 3, "rvq_pack_w_in: w_in_t must be (nq, D, d)");
@@ -442,71 +413,6 @@ Tensor rvq_pack_w_in(const Tensor& w_in_t) {
                               stream_of(w_in_t)),
            "vrvq_rvq_pack_w_in");
   return w3;
-}
-
-// rvq_encode from frame-major zt (B, T, D) (include/vrvq.h vrvq_rvq_encode_fm): the same six
-// outputs. Eager calls hand off through the library's own granule area; under stream capture
-// the workspace comes from the caching allocator (the graph's pool).
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> rvq_encode_fm(
-    const Tensor& zt, const Tensor& w3in, const Tensor& b_in, const Tensor& cb,
-    const Tensor& cbf, const Tensor& c2, const Tensor& w_out, const Tensor& b_out,
-    const Tensor& mcol, const Tensor& qb, const optional<Tensor>& imp, double level,
-    bool want_z_q_is, bool want_mask) {
-  check_pending_rvq_error();
-  check_t(zt, "zt");
-  TORCH_CHECK(zt.dim() == 3, "rvq_encode_fm: zt must be (B, T, D)");
-  check_on(w3in, zt, "w3in", at::kShort);
-  check_on(b_in, zt, "b_in");
-  check_on(cb, zt, "cb");
-  check_on(cbf, zt, "cbf");
-  check_on(c2, zt, "c2");
-  check_on(w_out, zt, "w_out");
-  check_on(b_out, zt, "b_out");
-  check_on(mcol, zt, "mcol");
-  check_on(qb, zt, "qb");
-  check_opt(imp, zt, "imp");
-  c10::DeviceGuard guard(zt.device());
-  const int64_t B = zt.size(0), T = zt.size(1), D = zt.size(2);
-  const int64_t nq = cb.size(0), N = cb.size(1), d = cb.size(2);
-  TORCH_CHECK(w_out.dim() == 3 && w_out.size(0) == nq && w_out.size(1) == D && w_out.size(2) == d,
-              "rvq_encode_fm: w_out must be (nq, D, d)");
-  TORCH_CHECK(b_out.numel() == nq * D && b_in.numel() == nq * d && c2.numel() == nq * N &&
-                  cbf.numel() == cb.numel(),
-              "rvq_encode_fm: stage weights do not match cb");
-  TORCH_CHECK(mcol.numel() == nq * nq * d * d && qb.numel() == nq * d,
-              "rvq_encode_fm: cross terms (rvq_cross_prep) do not match nq");
-  long long n3 = 0;
-  check_rc(vrvq_rvq_w_in_planes_size((int)nq, (int)D, (int)d, &n3), "vrvq_rvq_w_in_planes_size");
-  TORCH_CHECK(w3in.numel() == n3, "rvq_encode_fm: w3in must be rvq_pack_w_in(w_in_t)");
-  if (imp.has_value()) TORCH_CHECK(imp->numel() == B * T, "rvq_encode_fm: imp must hold B*T values");
-  Tensor codes = at::empty({B, nq, T}, zt.options().dtype(at::kLong));
-  Tensor latents = empty_f({B, nq * d, T}, zt);
-  Tensor loss_pf = empty_f({B, nq, T}, zt);
-  Tensor z_q_is = want_z_q_is ? empty_f({B, nq, D, T}, zt) : none_like(zt);
-  Tensor z_q = empty_f({B, D, T}, zt);
-  Tensor mask = want_mask ? empty_f({B, nq, T}, zt) : none_like(zt);
-  Tensor ws = none_like(zt);
-  const auto st = c10::hip::getCurrentHIPStream(zt.device().index());
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  TORCH_CHECK(hipStreamIsCapturing(st.stream(), &cs) == hipSuccess, "hipStreamIsCapturing");
-  if (cs != hipStreamCaptureStatusNone) {
-    long long ws_bytes = 0;
-    check_rc(vrvq_rvq_workspace_fm((int)B, (int)T, (int)nq, (int)N, &ws_bytes),
-             "vrvq_rvq_workspace_fm");
-    ws = at::empty({(ws_bytes + 3) / 4}, zt.options().dtype(at::kFloat));
-  }
-  check_rc(vrvq_rvq_encode_fm(zt.data_ptr<float>(), (int)B, (int)D, (int)T, (int)nq, (int)N,
-                              (int)d, reinterpret_cast<const uint16_t*>(w3in.data_ptr<int16_t>()),
-                              b_in.data_ptr<float>(), cb.data_ptr<float>(), cbf.data_ptr<float>(),
-                              c2.data_ptr<float>(), w_out.data_ptr<float>(),
-                              b_out.data_ptr<float>(), mcol.data_ptr<float>(),
-                              qb.data_ptr<float>(), fp(imp), (float)level,
-                              codes.data_ptr<int64_t>(), latents.data_ptr<float>(),
-                              loss_pf.data_ptr<float>(), opt_ptr(z_q_is), z_q.data_ptr<float>(),
-                              opt_ptr(mask), ws.numel() ? ws.data_ptr<float>() : nullptr,
-                              (long long)ws.numel() * 4, stream_of(zt)),
-           "vrvq_rvq_encode_fm");
-  return {codes, latents, loss_pf, z_q_is, z_q, mask};
 }
 
 // Snake1d -> WNConv1d (the encoder's last conv, models/dac_vrvq.py:33-34) with the in_proj of
@@ -1178,14 +1084,7 @@ TORCH_LIBRARY(vrvq, m) {
       "rvq_encode(Tensor z, Tensor w_in_t, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
       "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
       "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
-  m.def(
-      "snake_conv1d_fm(Tensor x, Tensor w_packed, int cout, int pad, int dil, Tensor? bias, "
-      "Tensor? alpha, Tensor? inv_alpha, Tensor? w_x3=None) -> Tensor");
   m.def("rvq_pack_w_in(Tensor w_in_t) -> Tensor");
-  m.def(
-      "rvq_encode_fm(Tensor zt, Tensor w3in, Tensor b_in, Tensor cb, Tensor cbf, Tensor c2, "
-      "Tensor w_out, Tensor b_out, Tensor mcol, Tensor qb, Tensor? imp, float level, "
-      "bool want_z_q_is, bool want_mask) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "snake_conv1d_proj(Tensor x, Tensor w_packed, int cout, int pad, int dil, Tensor? bias, "
       "Tensor? alpha, Tensor? inv_alpha, Tensor? w_x3, Tensor w3in, int nq, bool want_z) "
@@ -1252,9 +1151,7 @@ TORCH_LIBRARY(vrvq, m) {
   m.impl("rvq_cross_prep", &rvq_cross_prep); \
   m.impl("rvq_frag", &rvq_frag); \
   m.impl("rvq_encode", &rvq_encode); \
-  m.impl("snake_conv1d_fm", &snake_conv1d_fm); \
   m.impl("rvq_pack_w_in", &rvq_pack_w_in); \
-  m.impl("rvq_encode_fm", &rvq_encode_fm); \
   m.impl("snake_conv1d_proj", &snake_conv1d_proj); \
   m.impl("rvq_encode_part", &rvq_encode_part); \
   m.impl("rvq_check_error", &rvq_check_error); \

@@ -124,20 +124,6 @@ class WNConv1d(nn.Module):
                           out_snake=None if out_snake is None else out_snake.prepared(),
                           want_raw=want_raw, w_x3=self.prepared_x3())
 
-
-    def forward_fm(self, x: torch.Tensor, snake: Optional[Snake1d] = None) -> torch.Tensor:
-        """conv(snake(x)) + bias (stride 1) as a FRAME-MAJOR (B, T, Cout) tensor (the RVQ's
-        zt layout, include/vrvq.h vrvq_conv1d_fm); same values as forward."""
-        if self.stride[0] != 1:
-            raise RuntimeError("forward_fm: stride-1 convs only")
-        wp, _ = self.prepared()
-        alpha = inv = None
-        if snake is not None:
-            alpha, inv = snake.prepared()
-        return ops.conv1d_fm(x, wp, self.out_channels, self.kernel_size[0], self.padding[0],
-                             self.dilation[0], bias=self.bias.detach(), alpha=alpha,
-                             inv_alpha=inv, w_x3=self.prepared_x3())
-
     def forward_proj(self, x: torch.Tensor, w3in: torch.Tensor, nq: int,
                      snake: Optional[Snake1d] = None, want_z: bool = False):
         """conv(snake(x)) + bias (stride 1, 1024 outputs) with the in_proj of nq RVQ stages in

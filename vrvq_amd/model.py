@@ -34,12 +34,8 @@ class Encoder(nn.Module):
         self.block = nn.Sequential(*blocks)
         self.valid = False  # padding=False (CodecMixin.padding): unpadded convs
 
-    def forward(self, x, return_feat: bool = False, frame_major: bool = False,
-                project: Optional["_Stacked"] = None):
-        """frame_major: z comes back as the (B, D, T) view of a frame-major (B, T, D) tensor,
-        written that way by the last conv's epilogue (the layout the fused RVQ reads, see
-        _is_frame_major); the values are the same. project (a quantizer's stacked stage
-        weights): z comes back as a ProjectedZ -- the last conv's epilogue projects it onto every
+    def forward(self, x, return_feat: bool = False, project: Optional["_Stacked"] = None):
+        """project (a quantizer's stacked stage weights): z comes back as a ProjectedZ -- the last conv's epilogue projects it onto every
         stage's in_proj (include/vrvq.h vrvq_conv1d_proj) and z itself is not written."""
         if self.training:  # autograd path (vrvq_amd/train.py)
             if self.valid:
@@ -73,8 +69,6 @@ class Encoder(nn.Module):
             part, _ = self.block[n - 1].forward_proj(x, project.w3in(), nq, snake=self.block[n - 2])
             B = x.shape[0]
             out = ProjectedZ(part, B, self.block[n - 1].out_channels, part.shape[1] // B, nq)
-        elif frame_major:
-            out = self.block[n - 1].forward_fm(x, snake=self.block[n - 2]).transpose(1, 2)
         else:
             out = self.block[n - 1](x, snake=self.block[n - 2])
         return (out, feat) if return_feat else out
@@ -171,10 +165,8 @@ class VectorQuantize(nn.Module):
 # The eval encode hands z to the quantizer as its stage projections: the encoder's last conv
 # computes every stage's in_proj in its epilogue (vrvq_conv1d_proj) and the quantizer runs from
 # those partials (vrvq_rvq_encode_part: no z read, no projection in front of the chain).
-# VRVQ_RVQ_PROJ=0 (A/B): z frame-major and vrvq_rvq_encode_fm (chain parts project their own
-# frames), or, with VRVQ_RVQ_FM=0 as well, z (B, D, T) and vrvq_rvq_encode.
+# VRVQ_RVQ_PROJ=0 (A/B): z (B, D, T) and vrvq_rvq_encode.
 RVQ_PROJ = os.environ.get("VRVQ_RVQ_PROJ", "1") != "0"
-RVQ_FM = os.environ.get("VRVQ_RVQ_FM", "1") != "0"
 
 
 class ProjectedZ:
@@ -196,23 +188,14 @@ class ProjectedZ:
         return self.part.device
 
 
-def _is_frame_major(z: torch.Tensor) -> bool:
-    """z (B, D, T) is the transposed view of a contiguous (B, T, D) tensor."""
-    return z.dim() == 3 and not z.is_contiguous() and z.transpose(1, 2).is_contiguous()
-
-
 def _rvq_encode(z, st, **kw):
-    """ops.rvq_encode_part for a ProjectedZ, ops.rvq_encode_fm when z is a frame-major view,
-    else ops.rvq_encode."""
+    """ops.rvq_encode_part for a ProjectedZ, else ops.rvq_encode."""
     if isinstance(z, ProjectedZ):
         if z.nq != st.b_in.shape[0]:
             raise RuntimeError(f"ProjectedZ holds {z.nq} stages' projections, the quantizer "
                                f"runs {st.b_in.shape[0]}")
         return ops.rvq_encode_part(z.part, z.shape[2], st.b_in, st.cb, st.cbf, st.c2, st.w_out,
                                    st.b_out, st.mcol, st.qb, **kw)
-    if _is_frame_major(z):
-        return ops.rvq_encode_fm(z.transpose(1, 2), st.w3in(), st.b_in, st.cb, st.cbf, st.c2,
-                                 st.w_out, st.b_out, st.mcol, st.qb, **kw)
     return ops.rvq_encode(z.contiguous(), *st.codes_args(), **kw)
 
 
@@ -244,18 +227,22 @@ class _Stacked:
                 self.mcol, self.qb)
 
     def w3in(self):
-        """W_in planes of rvq_encode_fm (packed on first use)."""
+        """W_in planes of the encoder conv's projection epilogue (packed on first use)."""
         if getattr(self, "_w3in", None) is None:
             self._w3in = ops.rvq_pack_w_in(self.w_in_t)
         return self._w3in
 
     def prefix(self, n):
-        s = _Stacked.__new__(_Stacked)
-        s._w3in = None
-        for k in ("w_in_t", "b_in", "cb", "cbn", "cbf", "c2", "w_out", "b_out", "qb"):
-            setattr(s, k, getattr(self, k)[:n].contiguous())
-        s.mcol = self.mcol[:n, :n].contiguous()
-        return s
+        """The first n stages (a CBR prefix), built once per n."""
+        cache = self.__dict__.setdefault("_prefixes", {})
+        if n not in cache:
+            s = _Stacked.__new__(_Stacked)
+            s._w3in = None
+            for k in ("w_in_t", "b_in", "cb", "cbn", "cbf", "c2", "w_out", "b_out", "qb"):
+                setattr(s, k, getattr(self, k)[:n].contiguous())
+            s.mcol = self.mcol[:n, :n].contiguous()
+            cache[n] = s
+        return cache[n]
 
 
 def _stack_stages(quantizers, device):
@@ -573,15 +560,17 @@ class DAC_VRVQ(nn.Module, CodecMixin):
         caller does not need it (it is ~90 % of the quantizer's HBM traffic); the default keeps
         the reference's dict."""
         ev = not self.training and not self.encoder.valid
-        # the projection epilogue serves every stage: not a CBR prefix (n_quantizers < Nq)
-        proj = RVQ_PROJ and ev and (self.model_type == "VBR" or n_quantizers is None
-                                    or int(n_quantizers) >= self.n_codebooks)
+        # the projection epilogue computes the stages the quantizer runs: all of them, or a CBR
+        # prefix (n_quantizers < Nq; a VBR model raises for one in its quantizer)
+        proj = RVQ_PROJ and ev
         if proj:
-            z, feat = self.encoder(audio_data.contiguous(), return_feat=True,
-                                   project=self.quantizer.stacked())
+            st = self.quantizer.stacked()
+            nq = self.n_codebooks if n_quantizers is None else int(n_quantizers)
+            if self.model_type == "CBR" and 1 <= nq < self.n_codebooks:
+                st = st.prefix(nq)
+            z, feat = self.encoder(audio_data.contiguous(), return_feat=True, project=st)
         else:
-            z, feat = self.encoder(audio_data.contiguous(), return_feat=True,
-                                   frame_major=RVQ_FM and ev)
+            z, feat = self.encoder(audio_data.contiguous(), return_feat=True)
         if self.model_type == "CBR":
             return self.quantizer(z, n_quantizers)
         return self.quantizer(z, n_quantizers, feat, level, want_z_q_is=want_z_q_is)

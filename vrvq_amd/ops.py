@@ -115,18 +115,6 @@ def conv1d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, cout_pad: int, k:
     return _none(y) if out_snake is None else (_none(y), ys)
 
 
-def conv1d_fm(x: torch.Tensor, w_packed: torch.Tensor, cout: int, k: int, pad: int = 0,
-              dil: int = 1, bias: Optional[torch.Tensor] = None,
-              alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
-              w_x3: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """conv1d(snake(x)) + bias (stride 1) written FRAME-MAJOR: returns y (B, T, Cout), the
-    layout of rvq_encode_fm's zt (include/vrvq.h vrvq_conv1d_fm)."""
-    if w_packed.dim() != 3 or w_packed.shape[1] != k:
-        raise RuntimeError("conv1d_fm: w_packed must be (Cin, k, cout_pad)")
-    return _ops().snake_conv1d_fm(x, w_packed, int(cout), int(pad), int(dil), bias, alpha,
-                                  inv_alpha, w_x3)
-
-
 def conv1d_proj(x: torch.Tensor, w_packed: torch.Tensor, cout: int, k: int, w3in: torch.Tensor,
                 nq: int, pad: int = 0, dil: int = 1, bias: Optional[torch.Tensor] = None,
                 alpha: Optional[torch.Tensor] = None, inv_alpha: Optional[torch.Tensor] = None,
@@ -233,20 +221,9 @@ def rvq_encode(z, w_in_t, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
 
 
 def rvq_pack_w_in(w_in_t: torch.Tensor) -> torch.Tensor:
-    """W_in planes (bf16 x3 split, MFMA fragment order) for rvq_encode_fm, once per weight
+    """W_in planes (bf16 x3 split, MFMA fragment order) for conv1d_proj, once per weight
     version (include/vrvq.h vrvq_rvq_pack_w_in)."""
     return _ops().rvq_pack_w_in(w_in_t)
-
-
-def rvq_encode_fm(zt, w3in, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
-                  level: float = 1.0, want_z_q_is: bool = True, want_mask: bool = True):
-    """rvq_encode from frame-major zt (B, T, D): one launch per group of resident clips whose
-    chain parts project their own frames (include/vrvq.h vrvq_rvq_encode_fm). Same outputs as
-    rvq_encode."""
-    codes, lat, loss, zqis, zq, mask = _ops().rvq_encode_fm(zt, w3in, b_in, cb, cbf, c2, w_out,
-                                                          b_out, mcol, qb, imp, float(level),
-                                                          bool(want_z_q_is), bool(want_mask))
-    return codes, lat, loss, _none(zqis), zq, _none(mask)
 
 
 def rvq_encode_part(part, frames, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp=None,
@@ -454,24 +431,10 @@ def _register_fakes():
                 f32(z, (B, nq, T)), f32(z, (B, nq, D, T)) if want_z_q_is else none(z),
                 f32(z, (B, D, T)), f32(z, (B, nq, T)) if want_mask else none(z))
 
-    @reg("vrvq::snake_conv1d_fm")
-    def _(x, w_packed, cout, pad, dil, bias, alpha, inv_alpha, w_x3=None):
-        B, _c, tin = x.shape
-        return f32(x, (B, conv_out_len(tin, w_packed.shape[1], 1, pad, dil), cout))
-
     @reg("vrvq::rvq_pack_w_in")
     def _(w_in_t):
         nq = w_in_t.shape[0]
         return w_in_t.new_empty((32 * 3 * ((nq * 8 + 15) // 16) * 64 * 8,), dtype=torch.int16)
-
-    @reg("vrvq::rvq_encode_fm")
-    def _(zt, w3in, b_in, cb, cbf, c2, w_out, b_out, mcol, qb, imp, level, want_z_q_is,
-          want_mask):
-        B, T, D = zt.shape
-        nq, _n, d = cb.shape
-        return (zt.new_empty((B, nq, T), dtype=torch.int64), f32(zt, (B, nq * d, T)),
-                f32(zt, (B, nq, T)), f32(zt, (B, nq, D, T)) if want_z_q_is else none(zt),
-                f32(zt, (B, D, T)), f32(zt, (B, nq, T)) if want_mask else none(zt))
 
     @reg("vrvq::snake_conv1d_proj")
     def _(x, w_packed, cout, pad, dil, bias, alpha, inv_alpha, w_x3, w3in, nq, want_z):
