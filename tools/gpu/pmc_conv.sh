@@ -21,6 +21,9 @@ L[7]="--x3 --cin 384 --cout 384 --t 5568 --k 1 --res"
 L[8]="--x3 --cin 256 --cout 256 --t 5568 --k 1 --res"
 L[9]="--x3 --cin 512 --cout 1024 --t 696 --k 16 --stride 8"
 L[10]="--x3 --cin 192 --cout 96 --t 22272 --convt 2"
+L[11]="--x3 --cin 192 --cout 192 --t 22272 --k 1 --res"
+L[12]="--x3 --cin 768 --cout 768 --t 696 --k 1 --res"
+L[13]="--x3 --cin 192 --cout 192 --t 22272 --k 7 --dil 3"
 P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 P2="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"
 for i in ${LAYERS:-1 2 3 4 5 6 7 8 9 10}; do

@@ -9,7 +9,7 @@ a wide coalesced streaming read, so the fetch bytes are doubled; WRITE_SIZE is e
 
     python tools/pmc_traffic.py gpurun_out/<tag> profiles/<tag>_rvq_pmc.json [launches per call]
 
-The path is rvq_fm_kernel (the frame-major launch) or rvq_fused_kernel where a fused launch ran (one dispatch per <= 32 clips: the
+The path is rvq_pt_kernel (the launch from the conv's partials), rvq_fm_kernel (r05's frame-major launch) or rvq_fused_kernel where a fused launch ran (one dispatch per <= 32 clips: the
 third argument, default 1, scales a dispatch to one rvq_encode call), else the three kernels.
 """
 import collections
@@ -41,7 +41,9 @@ def main():
         kernels[k] = {"fetch_size_kib": f_kib, "write_size_kib": w_kib,
                       "fetch_bytes_corrected": 2 * f_kib * 1024, "write_bytes": w_kib * 1024,
                       "total": 2 * f_kib * 1024 + w_kib * 1024}
-    if "rvq_fm_kernel" in kernels:
+    if "rvq_pt_kernel" in kernels:  # the eval encode's launch from the conv's partials (r06)
+        path = ["rvq_pt_kernel"]
+    elif "rvq_fm_kernel" in kernels:
         path = ["rvq_fm_kernel"]
     elif "rvq_fused_kernel" in kernels:
         path = ["rvq_fused_kernel"]
