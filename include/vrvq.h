@@ -107,6 +107,23 @@ int vrvq_conv1d(const float* x, int batch, int cin, int tin, const float* alpha,
                 int epilogue, float* y, int tout, const float* alpha_out,
                 const float* inv_alpha_out, float* y_snake, vrvq_stream_t stream);
 
+/* vrvq_conv1d with a caller-owned workspace (device memory, >= the bytes vrvq_conv1d_workspace
+ * gives for the same shape, or NULL): the deep-K layers at tout <= 96 on the x3 path (the
+ * EncoderBlock's 512 -> 1024 stride-8 conv, the ImportanceSubnet's k3 convs, the decoder's
+ * first k7; models/dac_vrvq.py:32-35, 62-63, models/importance_subnet.py:38-45) then split
+ * their K loop into parts whose partial sums the workspace holds, added in part order by the
+ * epilogue launch. The part count depends on the layer's shape only (a clip's output does not
+ * change with the batch); the sums differ from vrvq_conv1d's (unsplit) by fp32 rounding.
+ * vrvq_conv1d_workspace: *bytes = 0 where no split applies (x3 = w_x3 != NULL). */
+int vrvq_conv1d_workspace(int batch, int cin, int tin, int cout, int k, int stride, int pad,
+                          int dil, int x3, long long* bytes);
+int vrvq_conv1d_ws(const float* x, int batch, int cin, int tin, const float* alpha,
+                   const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
+                   int cout_pad, int k, int stride, int pad, int dil, const float* bias,
+                   const float* residual, int epilogue, float* y, int tout,
+                   const float* alpha_out, const float* inv_alpha_out, float* y_snake,
+                   void* workspace, long long ws_bytes, vrvq_stream_t stream);
+
 /* fp32 convolution on the bf16 matrix cores (the "x3" path, vrvq_amd/csrc/conv_x3.h): with
  * w_x3 = vrvq_pack_x3_weight(w_packed) (null: the fp32-input MFMA path) the stride-1 convs
  * (k in {1, 2, 3, 7}; also the ConvTranspose1d and the ResidualUnit's k7) split both operands
@@ -128,11 +145,14 @@ int vrvq_pack_x3_weight(const float* w_packed, int cin, int k, int cout_pad, uin
  * 8 channel splits s and r < 8 nq -- vrvq_rvq_project's partials bit for bit (its x3 variant),
  * computed from the conv's accumulators, so the quantizer never reads z back (vrvq_rvq_encode_part
  * takes part). w3in = vrvq_rvq_pack_w_in(w_in_t). y (nullable) also receives z [B][1024][tout]
- * as vrvq_conv1d writes it. part: [8][B*tout][8 nq] fp32, 16-byte aligned. */
+ * as vrvq_conv1d writes it. part: [8][B*tout][8 nq] fp32, 16-byte aligned. workspace /
+ * ws_bytes: as vrvq_conv1d_ws (vrvq_conv1d_workspace of the same shape; with it the conv splits
+ * its K loop exactly as vrvq_conv1d_ws does, so z is the same bits either way). */
 int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, const float* alpha,
                      const float* inv_alpha, const float* w_packed, const uint16_t* w_x3, int cout,
                      int cout_pad, int k, int pad, int dil, const float* bias, float* y, int tout,
-                     const uint16_t* w3in, int nq, float* part, vrvq_stream_t stream);
+                     const uint16_t* w3in, int nq, float* part, void* workspace,
+                     long long ws_bytes, vrvq_stream_t stream);
 
 /* Pack a folded Conv1d weight w[Cout][Cin][k] into [Cin][k][cout_pad]. */
 int vrvq_pack_conv1d_weight(const float* w, int cout, int cin, int k, int cout_pad,

@@ -79,10 +79,11 @@ def test_argument_errors_raise_before_launch():
     assert lib.vrvq_rvq_encode_part(*([None] + [1] * 6 + [None] * 9 + [1.0] + [None] * 7 +
                                       [0, None])) == 10001
     assert lib.vrvq_conv1d_proj(None, 1, 1024, 87, None, None, None, None, 1024, 1024, 3, 1, 1,
-                                None, None, 87, None, 8, None, None) == 10001
+                                None, None, 87, None, 8, None, None, 0, None) == 10001
     # the projection epilogue serves the 1024-channel latent only
     assert lib.vrvq_conv1d_proj(p16 := ctypes.c_void_p(16), 1, 512, 87, None, None, p16, None,
-                                512, 512, 3, 1, 1, None, None, 87, p16, 8, p16, None) == 10002
+                                512, 512, 3, 1, 1, None, None, 87, p16, 8, p16, None, 0,
+                                None) == 10002
     with pytest.raises(RuntimeError, match="invalid argument"):
         _lib.call("vrvq_bpf", None, None, 1, 1, 1, None, None)
     # geometry mismatch (tout inconsistent with the conv formula)
@@ -92,6 +93,25 @@ def test_argument_errors_raise_before_launch():
     # producer-side snake without its alpha
     assert lib.vrvq_conv1d(p, 1, 4, 100, None, None, p, None, 4, 128, 7, 1, 3, 1, None, None,
                            0, None, 100, None, None, p, None) == 10001
+    # split-K workspace of the deep-K T <= 96 layers (conv.hip splitk_parts): S parts x B x
+    # M / 128 tiles x 128 x 96 fp32, S = 4 capped at chunks / 8 -- a function of the layer,
+    # not of the batch
+    def ws(*shape):
+        assert lib.vrvq_conv1d_workspace(*shape, ctypes.byref(n)) == 0
+        return n.value
+    tile = 128 * 96 * 4
+    assert ws(32, 512, 696, 1024, 16, 8, 4, 1, 1) == 4 * 32 * 8 * tile   # 512 -> 1024 s8
+    assert ws(1, 512, 696, 1024, 16, 8, 4, 1, 1) == 4 * 1 * 8 * tile
+    assert ws(32, 1024, 87, 1024, 3, 1, 1, 1, 1) == 4 * 32 * 8 * tile    # ImportanceSubnet k3
+    assert ws(32, 1024, 87, 512, 3, 1, 1, 1, 1) == 4 * 32 * 4 * tile
+    assert ws(32, 512, 87, 128, 3, 1, 1, 1, 1) == 4 * 32 * 1 * tile
+    assert ws(32, 128, 87, 128, 3, 1, 1, 1, 1) == 0                      # 8 chunks: none
+    assert ws(32, 1024, 87, 1536, 7, 1, 3, 1, 1) == 4 * 32 * 12 * tile   # decoder k7
+    assert ws(32, 128, 87, 32, 3, 1, 1, 1, 1) == 0                       # M < 128
+    assert ws(32, 1024, 87, 1024, 3, 1, 1, 1, 0) == 0                    # fp32-input path
+    assert ws(32, 384, 5568, 384, 7, 1, 3, 1, 1) == 0                    # long rows
+    assert lib.vrvq_conv1d_ws(p16, 1, 1024, 87, None, None, p16, p16, 1024, 1024, 3, 1, 1, 1,
+                              None, None, 0, p16, 87, None, None, None, p16, 16, None) == 10001
     # x3 weight size: chunks x 3 planes x padded octets x cout_pad x 8 bf16
     assert lib.vrvq_x3_weight_size(384, 7, 384, ctypes.byref(n)) == 0
     assert n.value == 48 * 3 * 8 * 384 * 8

@@ -3,6 +3,7 @@ plain PyTorch fp32 reference of each conv kernel. Needs an MI355X.
 
 Bar (north_star): integer codes and masks bit-exact; z_q / latents / waveform within 1e-4
 relative (max-abs normalised)."""
+import ctypes
 import os
 
 import numpy as np
@@ -382,6 +383,62 @@ def test_conv1d_strided_x3_vs_torch(case):
                         out_snake=(a_next, ops.snake_inv_alpha(a_next)), **kw)
     assert torch.equal(y4, y3)
     assert rel_err(ys.cpu().numpy(), _snake_ref(y3, a_next).cpu().numpy()) < 1e-6
+
+
+# The split-K T <= 96 layers (conv.hip splitk_parts: 128 x 96 tiles, the K chunks cut into parts
+# whose sums the workspace holds): (B, cin, cout, tin, k, stride, pad, dil, snake, residual, epi)
+SPLITK_CASES = [(3, 512, 1024, 696, 16, 8, 4, 1, True, False, 0),   # EncoderBlock 512 -> 1024 s8
+                (3, 1024, 1024, 87, 3, 1, 1, 1, True, False, 0),    # ImportanceSubnet in_block
+                (3, 1024, 512, 87, 3, 1, 1, 1, True, False, 0),
+                (3, 512, 128, 87, 3, 1, 1, 1, True, True, 0),
+                (3, 1024, 1536, 87, 7, 1, 3, 1, False, False, 0),   # decoder's first conv
+                (2, 1024, 1024, 40, 3, 1, 1, 1, True, False, 2)]
+
+
+@pytest.mark.parametrize("case", SPLITK_CASES)
+def test_conv1d_splitk_vs_torch_and_batch_invariant(case):
+    """The deep-K T <= 96 layers run split-K through the torch op (vrvq_conv1d_ws): against
+    torch fp64 at the x3 path's tolerance, within a small multiple of the unsplit x3 launch's
+    error (vrvq_conv1d, no workspace), and every clip bit-identical to the clip run alone (the
+    part count depends on the layer, not on the batch)."""
+    from vrvq_amd import _lib
+    B, cin, cout, T, k, s, p, d, use_snake, use_res, epi = case
+    need = ctypes.c_longlong(0)
+    _lib.call("vrvq_conv1d_workspace", B, cin, T, cout, k, s, p, d, 1, ctypes.byref(need))
+    assert need.value > 0, "the case must take the split-K path"
+    gen = torch.Generator(device="cpu").manual_seed(cin * 31 + cout + k)
+    x = (torch.rand(B, cin, T, generator=gen) - 0.5).to(DEV)
+    w = (torch.randn(cout, cin, k, generator=gen) / np.sqrt(cin * k)).to(DEV)
+    b = (torch.randn(cout, generator=gen) * 0.1).to(DEV)
+    alpha = (torch.rand(cin, generator=gen) * 1.5 + 0.5).to(DEV)
+    tout = (T + 2 * p - d * (k - 1) - 1) // s + 1
+    res = torch.randn(B, cout, tout, generator=gen).to(DEV) if use_res else None
+    xin = _snake_ref(x, alpha) if use_snake else x
+    ref = F.conv1d(xin.double(), w.double(), b.double(), stride=s, padding=p, dilation=d)
+    if use_res:
+        ref = res.double() + ref
+    ref = [ref, torch.tanh(ref), torch.sigmoid(ref)][epi].cpu().numpy()
+    wp, cout_pad = ops.pack_conv1d_weight(w)
+    w3 = ops.pack_x3_weight(wp, k) if s == 1 else ops.pack_x3_strided_weight(w, s)
+    inv = ops.snake_inv_alpha(alpha) if use_snake else None
+    kw = dict(bias=b, alpha=alpha if use_snake else None, inv_alpha=inv, residual=res,
+              epilogue=epi)
+    y = ops.conv1d(x, wp, cout, cout_pad, k, s, p, d, w_x3=w3, **kw)
+    e = rel_err(y.cpu().numpy(), ref)
+    assert e < 1e-5, e
+    # the unsplit x3 launch (C-ABI without a workspace)
+    y1 = torch.empty_like(y)
+    P = lambda v: ctypes.c_void_p(v.data_ptr()) if v is not None else None  # noqa: E731
+    _lib.call("vrvq_conv1d", P(x), B, cin, T, P(alpha if use_snake else None), P(inv), P(wp),
+              P(w3), cout, cout_pad, k, s, p, d, P(b), P(res), epi, P(y1), tout, None, None,
+              None, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    e1 = rel_err(y1.cpu().numpy(), ref)
+    assert e <= 4 * e1 + 2e-7, (e, e1)
+    for i in range(B):
+        kwi = dict(kw, residual=res[i:i + 1].contiguous() if use_res else None)
+        yi = ops.conv1d(x[i:i + 1].contiguous(), wp, cout, cout_pad, k, s, p, d, w_x3=w3, **kwi)
+        assert torch.equal(yi[0], y[i]), i
 
 
 @pytest.mark.parametrize("case", [(2, 1536, 768, 87, 8), (2, 768, 384, 100, 8),

@@ -129,9 +129,15 @@ def main():
     with torch.no_grad():
         m(torch.zeros(args.batch, 1, 44100), 44100, None, 1.0)
     rows = list(csv.DictReader(open(args.trace)))
-    conv = [r for r in rows if any(k in r["Kernel_Name"] for k in
-                                   ("conv_mfma_kernel", "conv_small", "conv_cout1", "conv_cin1",
-                                    "ru_fused_kernel"))]
+    conv = []
+    for r in rows:
+        if "conv_splitk_epilogue_kernel" in r["Kernel_Name"] and conv:
+            # a split-K layer (conv.hip launch_splitk): its K parts and their epilogue launch,
+            # stream-ordered, timed as one layer from the first start to the epilogue's end
+            conv[-1] = dict(conv[-1], End_Timestamp=r["End_Timestamp"])
+        elif any(k in r["Kernel_Name"] for k in ("conv_mfma_kernel", "conv_small", "conv_cout1",
+                                                   "conv_cin1", "ru_fused_kernel")):
+            conv.append(r)
     step = conv[-len(CALLS):]
     tot_t = tot_f = 0.0
     # %pk against the ceiling of the path the kernel runs: the x3 split-bf16 MFMA (template

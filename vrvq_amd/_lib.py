@@ -26,8 +26,11 @@ SIGNATURES = {
     "vrvq_codebook_prep": [_P, _I, _I, _P, _P, _P],
     "vrvq_conv1d": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
                     _P, _P, _P, _P],
+    "vrvq_conv1d_workspace": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "vrvq_conv1d_ws": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _I, _P,
+                       _I, _P, _P, _P, _P, ctypes.c_longlong, _P],
     "vrvq_conv1d_proj": [_P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _I,
-                         _P, _P],
+                         _P, _P, ctypes.c_longlong, _P],
     "vrvq_x3_weight_size": [_I, _I, _I, _P],
     "vrvq_pack_x3_weight": [_P, _I, _I, _I, _P, _P],
     "vrvq_pack_conv1d_weight": [_P, _I, _I, _I, _I, _P, _P],

@@ -24,13 +24,18 @@ namespace {
 using namespace vrvq_conv;
 
 template <int BM, int BN, int WM, int NW, int KS, bool X3, bool PH = false,
-          bool PAIR = x3_pair<KS, BM, BN>()>
+          bool PAIR = x3_pair<KS, BM, BN>(), bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW)
 __attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
 void conv_mfma_kernel(ConvArgs a) {
   using TC = TileCfg<BM, BN, WM, NW>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
+  int ks = 0;  // split-K part (SPLIT: the a.ks_split K parts of a tile are adjacent workgroups)
+  if (SPLIT) {
+    ks = bid % a.ks_split;
+    bid /= a.ks_split;
+  }
   int mt;
   if (a.mt_slow) {
     // M tile slowest: the workgroups in flight (a window of consecutive ids, spread over the 8
@@ -60,9 +65,68 @@ void conv_mfma_kernel(ConvArgs a) {
 #else
   constexpr bool SB = KS == 1 || (KS == 2 && BN == 128);
 #endif
-  if constexpr (X3) conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
-  else conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
+  if constexpr (X3) {
+    if constexpr (SPLIT) {
+      // split-K: this part's chunks, the raw sums to ks_part in fragment order (the tile's
+      // 64 NW threads x RM RN 16 floats, lane-contiguous: 256-B stores), no epilogue here
+      constexpr int CK = X3Cfg<KS, PAIR>::CK;
+      const int nch = (a.cin + CK - 1) / CK, per = (nch + a.ks_split - 1) / a.ks_split;
+      conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0, ks * per,
+                                                          min(nch, (ks + 1) * per));
+      constexpr int NR = TC::RM * TC::RN * 16;
+      const size_t tile = ((size_t)b * a.n_nt + nt) * a.n_mt + mt;
+      const size_t ntile = (size_t)gridDim.x / a.ks_split;
+      float* dst = a.ks_part + ((size_t)ks * ntile + tile) * (size_t)NR * 64 * NW +
+                   (threadIdx.x >> 6) * NR * 64 + (threadIdx.x & 63);
+#pragma unroll
+      for (int i = 0; i < TC::RM; ++i)
+#pragma unroll
+        for (int j = 0; j < TC::RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * TC::RN + j) * 16 + r) * 64] = acc[i][j][r];
+      return;
+    }
+    conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
+  } else {
+    conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
+  }
   conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, m0, n0);
+}
+
+// Split-K epilogue: one workgroup per tile (the block order of conv_mfma_kernel without its K
+// parts) adds the a.ks_split partial accumulators in part order -- a fixed order that depends on
+// the layer only, not on the batch -- and runs the tile's epilogue (bias, residual, activation,
+// next Snake) exactly as the unsplit kernel does.
+template <int BM, int BN, int WM, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_splitk_epilogue_kernel(ConvArgs a) {
+  using TC = TileCfg<BM, BN, WM, NW>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int bid = blockIdx.x;
+  const int mt = bid % a.n_mt;
+  bid /= a.n_mt;
+  const int nt = bid % a.n_nt;
+  const int b = bid / a.n_nt;
+  constexpr int NR = TC::RM * TC::RN * 16;
+  const size_t tile = blockIdx.x;  // ((b n_nt + nt) n_mt + mt): the split kernel's order
+  const size_t pstride = (size_t)gridDim.x * NR * 64 * NW;
+  const float* src = a.ks_part + tile * (size_t)NR * 64 * NW + (threadIdx.x >> 6) * NR * 64 +
+                     (threadIdx.x & 63);
+  f32x16 acc[TC::RM][TC::RN];
+#pragma unroll
+  for (int i = 0; i < TC::RM; ++i)
+#pragma unroll
+    for (int j = 0; j < TC::RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = src[((i * TC::RN + j) * 16 + r) * 64];
+  for (int s = 1; s < a.ks_split; ++s)
+#pragma unroll
+    for (int i = 0; i < TC::RM; ++i)
+#pragma unroll
+      for (int j = 0; j < TC::RN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[i][j][r] = acc[i][j][r] + src[s * pstride + ((i * TC::RN + j) * 16 + r) * 64];
+  conv_epilogue<BM, BN, WM, NW>(a, smem, acc, b, mt * BM, nt * BN);
 }
 
 // Small-Cout conv (Cout <= 8, stride 1): the decoder's 96->1 k7 + Tanh output layer and the
@@ -368,7 +432,7 @@ static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
 
 // The x3 launch of a tile (PAIR: its K-chunk form); VRVQ_ERR_UNSUPPORTED when its LDS does not
 // fit (the caller then takes the fp32-input loop).
-template <int BM, int BN, int WM, int NW, int KS, bool PAIR>
+template <int BM, int BN, int WM, int NW, int KS, bool PAIR, bool SPLIT = false>
 int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t st) {
   // the pair tiles' Snake table only when the staging applies a Snake (the producer-side
   // snake(x) inputs of the k7 layers need none: 3-6 KB of LDS back)
@@ -379,11 +443,11 @@ int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t
     if (a.psh) {  // strided conv through the phase-split view
       if (lx > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(
-            (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR>,
+            (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT>,
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
         if (e != hipSuccess) return (int)e;
       }
-      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR>),
+      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT>),
                          dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
       return vrvq_launch_status();
     }
@@ -391,11 +455,11 @@ int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t
   if (a.psh) return VRVQ_ERR_ARG;
   if (lx > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
-        (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR>,
+        (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR>),
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT>),
                      dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
   return vrvq_launch_status();
 }
@@ -556,9 +620,83 @@ static int conv_k1x3_192() {
   return v;
 }
 
+// Split-K for the deep-K, narrow-N layers at T <= 96 (the encoder's 512 -> 1024 s8 conv, the
+// importance subnet's k3 convs, the decoder's 1024 -> 1536 k7 at T = 87): their 32-wide tiles
+// re-streamed every M tile's whole weight block per 32 columns (50 MB of planes x 87 column
+// tiles for the s8 conv), and one 96-wide tile per clip gives too few workgroups to hide a
+// 128-chunk serial K loop. Here: 128 x 96 tiles (one per clip: the weight block read once per
+// clip) with the channel chunks cut into S = 4 parts (at least 8 chunks a part) -- a function of
+// the layer only, so a clip's sums do not change with the batch. Per layer at B = 32
+// (profiles/r06ks_splitk_sweep.txt, S = none / 2 / 3 / 4 / 6 / 8): 512 -> 1024 s8 645 / 441 /
+// 469 / 445 / 462 / 455 us, 1024 -> 1024 k3 182 / 140 / 169 / 143 / 155 / 159, 1024 -> 512 k3
+// 124 / 95 / 91 / 79 / 94 / 85, 512 -> 128 k3 48 -> 38 (S <= 4: 32 chunks), 1024 -> 1536 k7
+// 518 / 525 / 530 / 467 / 496 / 479: S = 4 is within 1 % of the best everywhere.
+// Tuning override VRVQ_CONV_SPLITK=0 (off) | S (forced part count).
+static int conv_splitk_env() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_SPLITK");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
+// K parts of a layer (0: none). ks = the GEMM's taps (2 for the phase-split view), cin = the
+// GEMM's channels (the view's for a strided conv). The same for vrvq_conv1d_proj (the encoder's
+// last conv, whose shape the ImportanceSubnet's first conv shares): its projection epilogue then
+// runs in the split-K epilogue launch, on the same z bits as the plain conv's.
+int splitk_parts(int M, int cin, int ng, int ks, bool psh, bool up, bool x3) {
+  const int env = conv_splitk_env();
+  if (env == 0 || !x3 || up || ng > 96 || M % 128 != 0) return 0;
+  if (!(ks == 3 || ks == 7 || (ks == 2 && psh))) return 0;
+  const int ck = ks == 2 ? X3Cfg<2, true>::CK : ks == 3 ? X3Cfg<3>::CK : X3Cfg<7>::CK;
+  if (ks == 2 && cin % ck != 0) return 0;
+  const int nch = (cin + ck - 1) / ck;
+  int S = env > 0 ? env : 4;
+  if (S > nch / 8) S = nch / 8;
+  return S >= 2 ? S : 0;
+}
+
+size_t splitk_bytes(int S, int M, int ng, int batch) {
+  return S ? (size_t)S * batch * (M / 128) * ((ng + 95) / 96) * 128 * 96 * sizeof(float) : 0;
+}
+
+template <int KS>
+int launch_splitk(const ConvArgs& a0, int batch, int S, hipStream_t st) {
+  if constexpr (KS == 2 || KS == 3 || KS == 7) {
+    ConvArgs a = a0;
+    a.ks_split = S;
+    a.n_mt = a.M / 128;
+    a.n_nt = (a.ng + 95) / 96;
+    a.mt_slow = 0;
+    if (a.m_pad < a.n_mt * 128) return VRVQ_ERR_ARG;
+    const int XW = 95 + (KS - 1) * a.dil + 1;
+    constexpr int XW_MAX = 95 + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
+    if (XW > XW_MAX) return VRVQ_ERR_UNSUPPORTED;
+    size_t epi = (size_t)128 * EpiCfg<128, 96, 1>::BNP * sizeof(float);
+    if (a.pj_part && epi < (size_t)PJE_LDS) epi = PJE_LDS;
+    const long long tiles = (long long)a.n_mt * a.n_nt * batch;
+    if (tiles * S > 0x7fffffffLL) return VRVQ_ERR_ARG;
+    const int rc = launch_x3<128, 96, 4, 4, KS, KS == 2, true>(a, XW, epi, tiles * S, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL((conv_splitk_epilogue_kernel<128, 96, 4, 4>), dim3((unsigned)tiles),
+                       dim3(256), epi, st, a);
+    return vrvq_launch_status();
+  } else {
+    (void)a0; (void)batch; (void)S; (void)st;
+    return VRVQ_ERR_UNSUPPORTED;
+  }
+}
+
 // Tile choice: BM from the GEMM row count, BN minimising padded columns (prefer wide).
 template <int KS>
 int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
+  if (a.ks_part != nullptr) {
+    const int S = splitk_parts(a.M, a.cin, a.ng, KS, a.psh > 0, a.up > 0, a.w3 != nullptr);
+    if (S > 0) {
+      const int rc = launch_splitk<KS>(a, batch, S, st);
+      if (rc != VRVQ_ERR_UNSUPPORTED) return rc;
+    }
+  }
   auto waste = [&](int bn) { return ((a.ng + bn - 1) / bn) * bn - a.ng; };
   int bn;
   if (a.ng <= 32) bn = 32;
@@ -781,6 +919,35 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
                            const float* residual, int epilogue, float* y, int tout,
                            const float* alpha_out, const float* inv_alpha_out, float* y_snake,
                            vrvq_stream_t stream) {
+  return vrvq_conv1d_ws(x, batch, cin, tin, alpha, inv_alpha, w_packed, w_x3, cout, cout_pad, k,
+                        stride, pad, dil, bias, residual, epilogue, y, tout, alpha_out,
+                        inv_alpha_out, y_snake, nullptr, 0, stream);
+}
+
+extern "C" int vrvq_conv1d_workspace(int batch, int cin, int tin, int cout, int k, int stride,
+                                     int pad, int dil, int x3, long long* bytes) {
+  VRVQ_CHECK_ARG(bytes && batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && stride > 0 &&
+                 dil > 0 && pad >= 0);
+  const long long tout = ((long long)tin + 2LL * pad - (long long)dil * (k - 1) - 1) / stride + 1;
+  VRVQ_CHECK_ARG(tout > 0);
+  int S = 0;
+  if (stride > 1) {  // the phase-split view (vrvq_conv1d: k = 2 stride, power-of-two stride)
+    if (x3 && k == 2 * stride && (stride & (stride - 1)) == 0 && pad < stride)
+      S = splitk_parts(cout, cin * stride, (int)tout, 2, true, false, true);
+  } else {
+    S = splitk_parts(cout, cin, (int)tout, k, false, false, x3 != 0);
+  }
+  *bytes = (long long)splitk_bytes(S, cout, (int)tout, batch);
+  return 0;
+}
+
+extern "C" int vrvq_conv1d_ws(const float* x, int batch, int cin, int tin, const float* alpha,
+                              const float* inv_alpha, const float* w_packed,
+                              const uint16_t* w_x3, int cout, int cout_pad, int k, int stride,
+                              int pad, int dil, const float* bias, const float* residual,
+                              int epilogue, float* y, int tout, const float* alpha_out,
+                              const float* inv_alpha_out, float* y_snake, void* workspace,
+                              long long ws_bytes, vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(x && w_packed && (y || y_snake));
   VRVQ_CHECK_ARG(y_snake == nullptr || (alpha_out && inv_alpha_out));
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && stride > 0 &&
@@ -801,6 +968,14 @@ extern "C" int vrvq_conv1d(const float* x, int batch, int cin, int tin, const fl
     while ((1 << a.ssh) < stride) ++a.ssh;
   a.ylen = tout; a.epi = epilogue;
   a.w3 = reinterpret_cast<const unsigned*>(w_x3);
+  if (workspace != nullptr) {
+    long long need = 0;
+    const int rc = vrvq_conv1d_workspace(batch, cin, tin, cout, k, stride, pad, dil,
+                                         w_x3 != nullptr, &need);
+    if (rc) return rc;
+    VRVQ_CHECK_ARG(ws_bytes >= need);
+    if (need > 0) a.ks_part = static_cast<float*>(workspace);
+  }
   if (w_x3 != nullptr && stride > 1) {
     // strided conv on the x3 loop: a stride-1 k = 2 conv over the phase-split view of x
     // (conv_core.h ConvArgs::psh); w_x3 holds the planes of W'[co][c*s + r][j] = W[co][c][j*s + r]
@@ -828,8 +1003,8 @@ extern "C" int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, con
                                 const float* inv_alpha, const float* w_packed,
                                 const uint16_t* w_x3, int cout, int cout_pad, int k, int pad,
                                 int dil, const float* bias, float* y, int tout,
-                                const uint16_t* w3in, int nq, float* part,
-                                vrvq_stream_t stream) {
+                                const uint16_t* w3in, int nq, float* part, void* workspace,
+                                long long ws_bytes, vrvq_stream_t stream) {
   VRVQ_CHECK_ARG(x && w_packed && w3in && part);
   VRVQ_CHECK_ARG(batch > 0 && cin > 0 && tin > 0 && cout > 0 && k > 0 && dil > 0 && pad >= 0 &&
                  tout > 0 && nq > 0);
@@ -850,6 +1025,14 @@ extern "C" int vrvq_conv1d_proj(const float* x, int batch, int cin, int tin, con
   a.pj_part = part;
   a.pj_nq = nq;
   a.pj_nf = batch * tout;
+  if (workspace != nullptr) {  // split-K as vrvq_conv1d_ws (same shape, same parts)
+    long long need = 0;
+    const int rc = vrvq_conv1d_workspace(batch, cin, tin, cout, k, 1, pad, dil, w_x3 != nullptr,
+                                         &need);
+    if (rc) return rc;
+    VRVQ_CHECK_ARG(ws_bytes >= need);
+    if (need > 0) a.ks_part = static_cast<float*>(workspace);
+  }
   // the MFMA tiles only (their epilogue owns the projection); every 1024-row tile is 128 rows
   return dispatch_ks(k, a, batch, as_stream(stream));
 }

@@ -44,6 +44,12 @@ struct ConvArgs {
   float* pj_part;
   int pj_nq;
   int pj_nf;               // frames of the whole call (B * ng): the partials' split stride
+  // split-K over the channel chunks (the deep-K, narrow-N T <= 96 layers, vrvq_conv1d_ws):
+  // workgroup (tile, s) sums chunks [s per, (s + 1) per) of its tile into ks_part (fragment
+  // order), conv_splitk_epilogue_kernel adds the ks_split partials in s order and runs the
+  // epilogue. ks_split <= 1: none.
+  int ks_split;
+  float* ks_part;
 };
 
 // v = h + m + l exactly (RNE at each step; conv_x3.h split3x2), two values per call

@@ -121,7 +121,7 @@ template <int BM, int BN, int WM, int NW, int KS, bool PH = false,
 __device__ __forceinline__ void conv_mainloop_x3(
     const ConvArgs& a, float* smem,
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
-    int n0) {
+    int n0, int kc0 = 0, int kc1 = 0x7fffffff) {
   using TC = TileCfg<BM, BN, WM, NW>;
   static_assert(!PAIR || ((KS == 7 || KS == 1) && !PH) || KS == 2,
                 "pair chunks: k7 / k1 stride-1 windows, the 2-tap GEMMs");
@@ -270,7 +270,8 @@ __device__ __forceinline__ void conv_mainloop_x3(
     }
   };
 
-  const int nchunks = (a.cin + CK - 1) / CK;
+  // channel chunks [kc0, kc1) of the K loop (split-K: one part of them)
+  const int nchunks = min((a.cin + CK - 1) / CK, kc1);
   const int col = wn * TN + lr;
   auto rd_at = [&](const u32x4* ws, const u32x4* xs, int q, u32x4 (&av)[3][RM], u32x4 (&bv)[3][RN]) {
     // octet slot o = 2 q + lh: (tap, channel octet) in tap-major order; a pair chunk's slot
@@ -340,12 +341,12 @@ __device__ __forceinline__ void conv_mainloop_x3(
     }
   }
   int cur = 0;
-  load_w(0);
-  load_x(0);
+  load_w(kc0);
+  load_x(kc0 * CK);
   store_w(sbase);
-  store_x(sbase, 0);
+  store_x(sbase, kc0 * CK);
   __syncthreads();
-  for (int c = 0; c < nchunks; ++c) {
+  for (int c = kc0; c < nchunks; ++c) {
     // Next chunk's loads in flight during this chunk's MFMAs. Unconditional (the last chunk
     // reloads itself into the idle stage): under `if (more)` the compiler sinks the loads past
     // the MFMAs into the store block, their only user.

@@ -214,12 +214,19 @@ std::tuple<Tensor, Tensor> snake_conv1d(const Tensor& x, const Tensor& w_packed,
   // view channels, 2 taps; include/vrvq.h vrvq_conv1d)
   const uint16_t* w3 = stride > 1 ? x3_ptr(w_x3, x, cin * stride, 2, cout_pad)
                                   : x3_ptr(w_x3, x, cin, k, cout_pad);
-  check_rc(vrvq_conv1d(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                       fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout, (int)cout_pad,
-                       (int)k, (int)stride, (int)pad, (int)dil, fp(bias), fp(residual),
-                       (int)epilogue, y.numel() ? y.data_ptr<float>() : nullptr, (int)tout,
-                       fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys), stream_of(x)),
-           "vrvq_conv1d");
+  // split-K workspace of the deep-K T <= 96 layers (caching allocator: capture-safe)
+  long long ws_bytes = 0;
+  check_rc(vrvq_conv1d_workspace((int)B, (int)cin, (int)tin, (int)cout, (int)k, (int)stride,
+                                 (int)pad, (int)dil, w3 != nullptr, &ws_bytes),
+           "vrvq_conv1d_workspace");
+  Tensor ws = ws_bytes > 0 ? at::empty({(ws_bytes + 3) / 4}, x.options()) : Tensor();
+  check_rc(vrvq_conv1d_ws(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
+                          fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
+                          (int)cout_pad, (int)k, (int)stride, (int)pad, (int)dil, fp(bias),
+                          fp(residual), (int)epilogue, y.numel() ? y.data_ptr<float>() : nullptr,
+                          (int)tout, fp(alpha_out), fp(inv_alpha_out), opt_ptr(ys),
+                          ws_bytes > 0 ? ws.data_ptr() : nullptr, ws_bytes, stream_of(x)),
+           "vrvq_conv1d_ws");
   return {y, ys};
 }
 
@@ -445,12 +452,19 @@ std::tuple<Tensor, Tensor> snake_conv1d_proj(const Tensor& x, const Tensor& w_pa
   TORCH_CHECK(w3in.numel() == n3, "conv1d_proj: w3in must be rvq_pack_w_in(w_in_t) of nq stages");
   Tensor part = empty_f({8, B * tout, nq * 8}, x);
   Tensor z = want_z ? empty_f({B, cout, tout}, x) : none_like(x);
+  const uint16_t* w3 = x3_ptr(w_x3, x, cin, k, cout_pad);
+  // the split-K workspace of the shape (as snake_conv1d: the same z bits as the plain conv)
+  long long ws_bytes = 0;
+  check_rc(vrvq_conv1d_workspace((int)B, (int)cin, (int)tin, (int)cout, (int)k, 1, (int)pad,
+                                 (int)dil, w3 != nullptr, &ws_bytes),
+           "vrvq_conv1d_workspace");
+  Tensor ws = ws_bytes > 0 ? at::empty({(ws_bytes + 3) / 4}, x.options()) : Tensor();
   check_rc(vrvq_conv1d_proj(x.data_ptr<float>(), (int)B, (int)cin, (int)tin, fp(alpha),
-                            fp(inv_alpha), w_packed.data_ptr<float>(),
-                            x3_ptr(w_x3, x, cin, k, cout_pad), (int)cout, (int)cout_pad, (int)k,
-                            (int)pad, (int)dil, fp(bias), opt_ptr(z), (int)tout,
-                            reinterpret_cast<const uint16_t*>(w3in.data_ptr<int16_t>()), (int)nq,
-                            part.data_ptr<float>(), stream_of(x)),
+                            fp(inv_alpha), w_packed.data_ptr<float>(), w3, (int)cout,
+                            (int)cout_pad, (int)k, (int)pad, (int)dil, fp(bias), opt_ptr(z),
+                            (int)tout, reinterpret_cast<const uint16_t*>(w3in.data_ptr<int16_t>()),
+                            (int)nq, part.data_ptr<float>(),
+                            ws_bytes > 0 ? ws.data_ptr() : nullptr, ws_bytes, stream_of(x)),
            "vrvq_conv1d_proj");
   return {part, z};
 }
