@@ -24,7 +24,7 @@ namespace {
 using namespace vrvq_conv;
 
 template <int BM, int BN, int WM, int NW, int KS, bool X3, bool PH = false,
-          bool PAIR = x3_pair<KS, BM, BN>(), bool SPLIT = false>
+          bool PAIR = x3_pair<KS, BM, BN>(), bool SPLIT = false, bool XPF = false>
 __global__ __launch_bounds__(64 * NW)
 __attribute__((amdgpu_waves_per_eu(X3 && x3_stages<BM, BN>() == 1 ? 2 : 1)))
 void conv_mfma_kernel(ConvArgs a) {
@@ -63,7 +63,8 @@ void conv_mfma_kernel(ConvArgs a) {
 #ifdef VRVQ_X3_SB_ALL  // A/B build
   constexpr bool SB = true;
 #else
-  constexpr bool SB = KS == 1 || (KS == 2 && BN == 128);
+  // (XPF: the x prefetch registers take the place of the second operand set)
+  constexpr bool SB = KS == 1 || (KS == 2 && BN == 128) || XPF;
 #endif
   if constexpr (X3) {
     if constexpr (SPLIT) {
@@ -86,7 +87,7 @@ void conv_mfma_kernel(ConvArgs a) {
           for (int r = 0; r < 16; ++r) dst[((i * TC::RN + j) * 16 + r) * 64] = acc[i][j][r];
       return;
     }
-    conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0);
+    conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB, XPF>(a, smem, acc, b, m0, n0);
   } else {
     conv_mainloop<BM, BN, WM, NW, KS>(a, smem, acc, b, m0, n0);
   }
@@ -424,6 +425,16 @@ static int x3_rule() {
   return v;
 }
 
+// The 64 x 256 pair k7 tiles with the next chunk's x window prefetched into registers during the
+// MFMAs (conv_x3.h XPF). Tuning override VRVQ_CONV_XPF=0 | 1.
+static int conv_x3_xpf() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_XPF");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
   (void)a;
   if (x3_rule() == 0) return true;
@@ -432,7 +443,7 @@ static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
 
 // The x3 launch of a tile (PAIR: its K-chunk form); VRVQ_ERR_UNSUPPORTED when its LDS does not
 // fit (the caller then takes the fp32-input loop).
-template <int BM, int BN, int WM, int NW, int KS, bool PAIR, bool SPLIT = false>
+template <int BM, int BN, int WM, int NW, int KS, bool PAIR, bool SPLIT = false, bool XPF = false>
 int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t st) {
   // the pair tiles' Snake table only when the staging applies a Snake (the producer-side
   // snake(x) inputs of the k7 layers need none: 3-6 KB of LDS back)
@@ -443,11 +454,11 @@ int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t
     if (a.psh) {  // strided conv through the phase-split view
       if (lx > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(
-            (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT>,
+            (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT, XPF>,
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
         if (e != hipSuccess) return (int)e;
       }
-      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT>),
+      hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, true, PAIR, SPLIT, XPF>),
                          dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
       return vrvq_launch_status();
     }
@@ -455,11 +466,11 @@ int launch_x3(const ConvArgs& a, int XW, size_t epi, long long nblk, hipStream_t
   if (a.psh) return VRVQ_ERR_ARG;
   if (lx > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
-        (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT>,
+        (const void*)conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT, XPF>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lx);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT>),
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, NW, KS, true, false, PAIR, SPLIT, XPF>),
                      dim3((unsigned)nblk), dim3(64 * NW), lx, st, a);
   return vrvq_launch_status();
 }
@@ -492,8 +503,13 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
         x3_tile_ok(BM, BN, KS, a)) {
       // pair tiles (conv_x3.h) need whole K-chunks: other Cin run the tile on plain chunks
       int rc = VRVQ_ERR_UNSUPPORTED;
-      if (x3_pair<KS, BM, BN>() && a.cin % X3Cfg<KS, true>::CK == 0)
-        rc = launch_x3<BM, BN, WM, NW, KS, x3_pair<KS, BM, BN>()>(a, XW, epi, nblk, st);
+      if (x3_pair<KS, BM, BN>() && a.cin % X3Cfg<KS, true>::CK == 0) {
+        constexpr bool kXpf = KS == 7 && x3_pair<KS, BM, BN>();  // the 64 x 256 pair k7 tile
+        if (kXpf && conv_x3_xpf())
+          rc = launch_x3<BM, BN, WM, NW, KS, x3_pair<KS, BM, BN>(), false, kXpf>(a, XW, epi, nblk, st);
+        else
+          rc = launch_x3<BM, BN, WM, NW, KS, x3_pair<KS, BM, BN>()>(a, XW, epi, nblk, st);
+      }
       else
         rc = launch_x3<BM, BN, WM, NW, KS, false>(a, XW, epi, nblk, st);
       if (rc != VRVQ_ERR_UNSUPPORTED) return rc;

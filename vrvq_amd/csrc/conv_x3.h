@@ -116,8 +116,11 @@ struct X3W {
 // instantiations keep their plain window addressing).
 // SB: single-buffered LDS operand reads in the chunk's MFMA loop (one step's operands live
 // instead of two: fewer registers, so more workgroups per CU where the registers were the limit)
+// XPF (single-stage loop only): the next chunk's x window is loaded into registers BEFORE the
+// chunk's MFMAs (raw fp32, zeroed / Snake / split at the store as before), so only the weight
+// planes' L2 round trip stays between the two barriers of the refill.
 template <int BM, int BN, int WM, int NW, int KS, bool PH = false,
-          bool PAIR = x3_pair<KS, BM, BN>(), bool SB = false>
+          bool PAIR = x3_pair<KS, BM, BN>(), bool SB = false, bool XPF = false>
 __device__ __forceinline__ void conv_mainloop_x3(
     const ConvArgs& a, float* smem,
     f32x16 (&acc)[TileCfg<BM, BN, WM, NW>::RM][TileCfg<BM, BN, WM, NW>::RN], int b, int m0,
@@ -356,6 +359,9 @@ __device__ __forceinline__ void conv_mainloop_x3(
       load_w(cn);
       load_x(cn * CK);
       __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (XPF) {
+      load_x(cn * CK);  // unconditional (the last chunk reloads itself): see above
+      __builtin_amdgcn_sched_barrier(0);
     }
     chunk_mma(reinterpret_cast<const u32x4*>(sbase + cur * STG),
               reinterpret_cast<const u32x4*>(sbase + cur * STG + WB));
@@ -368,7 +374,7 @@ __device__ __forceinline__ void conv_mainloop_x3(
       __syncthreads();  // every wave done with the stage
       if (c + 1 < nchunks) {
         load_w(cn);
-        load_x(cn * CK);
+        if constexpr (!XPF) load_x(cn * CK);
         // every load of the refill in flight before the first store waits on one (else the
         // x loads are issued only after the W stores: two memory round trips per chunk)
         __builtin_amdgcn_sched_barrier(0);
