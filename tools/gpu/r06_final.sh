@@ -17,4 +17,5 @@ has prof && run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T
 has cfg3 && run cfg3 300 python bench.py --batch 64 --n-codebooks 32 --steps 10 --warmup 2 --no-cpu-baseline
 has sweep && run sweep 300 python bench.py --sweep --steps 10 --warmup 2 --no-cpu-baseline
 has train && run train 400 python bench.py --train --steps 3 --warmup 2
+has bench10 && run bench10 400 python bench.py --clip-seconds 10 --batch 1 --sweep --steps 5 --warmup 2 --no-cpu-baseline
 exit 0
