@@ -158,18 +158,37 @@ __global__ __launch_bounds__(256) void conv_small_cout_kernel(ConvArgs a, int ks
 #pragma unroll
   for (int c = 0; c < COUT; ++c) acc[c] = 0.0f;
 
+  // staged positions: the window of this block's output positions only (short rows: T = 87)
+  const int pmax = min(XW, a.ng - t0 + (ks - 1) * a.dil);
   for (int ci0 = 0; ci0 < a.cin; ci0 += SMALL_SC) {
     const int nc = min(SMALL_SC, a.cin - ci0);
-    for (int e = tid; e < nc * XW; e += 256) {
-      const int cl = e / XW, p = e - cl * XW;
-      const int ci = ci0 + cl;
-      const int t = t0 - a.pad + p;
-      float v = 0.0f;
-      if (t >= 0 && t < a.tin) {
-        v = xb[(size_t)ci * a.tin + t];
-        if (a.alpha) v = snake_act(v, a.alpha[ci], a.inv_alpha[ci]);
+    const int total = nc * pmax;
+    // eight loads in flight per thread from clamped addresses, then the zeroing / Snake / LDS
+    // stores (a load under the range branch made every iteration wait for its own load)
+    for (int e0 = tid; e0 < total; e0 += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(e0 + u * 256, total - 1);
+        const int cl = e / pmax, p = e - cl * pmax;
+        const int tc = min(max(t0 - a.pad + p, 0), a.tin - 1);
+        v[u] = xb[(size_t)(ci0 + cl) * a.tin + tc];
       }
-      xs[cl * XW + p] = v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256;
+        if (e < total) {
+          const int cl = e / pmax, p = e - cl * pmax;
+          const int ci = ci0 + cl;
+          const int t = t0 - a.pad + p;
+          float x = 0.0f;
+          if (t >= 0 && t < a.tin) {
+            x = v[u];
+            if (a.alpha) x = snake_act(x, a.alpha[ci], a.inv_alpha[ci]);
+          }
+          xs[cl * XW + p] = x;
+        }
+      }
     }
     __syncthreads();
     for (int cl = 0; cl < nc; ++cl) {
@@ -783,6 +802,7 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
       convt_96()) {
     // x3 polyphase ConvTranspose1d with 96-row multiples (192 -> 96 s2: M = 192): 96-row
     // tiles on the pair chunks (two workgroups per CU) instead of the two-stage 192 x 128 tile
+    // (single-stage 192 x 64 tiles, x read once: 981-988 vs 942-954 us, r06t_convt_layers.txt)
     return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
   }
   if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
