@@ -36,17 +36,10 @@ void conv_mfma_kernel(ConvArgs a) {
     ks = bid % a.ks_split;
     bid /= a.ks_split;
   }
-  int mt;
-  if (a.mt_slow) {
-    // M tile slowest: the workgroups in flight (a window of consecutive ids, spread over the 8
-    // XCDs) all use one weight tile, so each XCD's L2 holds it instead of every M tile's
-    const int per = (int)gridDim.x / a.n_mt;
-    mt = bid / per;
-    bid -= mt * per;
-  } else {
-    mt = bid % a.n_mt;
-    bid /= a.n_mt;
-  }
+  // M tile fastest (an M-tile-slowest order, all CUs on one weight tile for L2 reuse, measured
+  // no faster in r02: the weight tiles are not what limits)
+  const int mt = bid % a.n_mt;
+  bid /= a.n_mt;
   const int nt = bid % a.n_nt;
   const int b = bid / a.n_nt;
   const int m0 = mt * BM;
@@ -413,6 +406,17 @@ static int convt_96() {
   return v;
 }
 
+// The 64 x 256 pair k7 tiles with the next chunk's x window prefetched into registers during the
+// MFMAs (conv_x3.h XPF; profiles/r06x_xpf_layers.txt: 1-3.5 % per layer). Tuning override
+// VRVQ_CONV_XPF=0 | 1.
+static int conv_x3_xpf() {
+  static const int v = [] {
+    const char* e = getenv("VRVQ_CONV_XPF");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // Cin = 1 convs on conv_cin1_stream_kernel (default) | VRVQ_CONV_CIN1=0: the fp32 MFMA tile
 static int cin1_stream() {
   static const int v = [] {
@@ -422,43 +426,7 @@ static int cin1_stream() {
   return v;
 }
 
-// tuning override: VRVQ_CONV_MTSLOW=1 (M tile slowest) | 0 (default: 495.1 vs 492.6
-// audio-sec/s with it, profiles/r02zd_conv_ab.txt — the weight tiles are not what limits)
-static int conv_mt_slow() {
-  static const int v = [] {
-    const char* e = getenv("VRVQ_CONV_MTSLOW");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 
-// Where the bf16x3 path runs when a pre-split weight is given: every eligible stride-1 tile
-// (VRVQ_CONV_X3_RULE=1: the rule of the first x3 version, which lost on the 192 x 64 k = 1
-// tile before the single-stage, two-workgroups-per-CU loop). Per layer at B = 32:
-// profiles/r02zd_x3_layers.txt (first version), profiles/r02zg_layer_table.txt (this one).
-static int x3_rule() {
-  static const int v = [] {
-    const char* e = getenv("VRVQ_CONV_X3_RULE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// The 64 x 256 pair k7 tiles with the next chunk's x window prefetched into registers during the
-// MFMAs (conv_x3.h XPF). Tuning override VRVQ_CONV_XPF=0 | 1.
-static int conv_x3_xpf() {
-  static const int v = [] {
-    const char* e = getenv("VRVQ_CONV_XPF");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-static bool x3_tile_ok(int bm, int bn, int ks, const ConvArgs& a) {
-  (void)a;
-  if (x3_rule() == 0) return true;
-  return !(ks == 1 && bm == 192 && bn == 64);
-}
 
 // The x3 launch of a tile (PAIR: its K-chunk form); VRVQ_ERR_UNSUPPORTED when its LDS does not
 // fit (the caller then takes the fp32-input loop).
@@ -515,11 +483,9 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   const long long nblk = (long long)a.n_mt * a.n_nt * batch;
   if (nblk <= 0 || nblk > 0x7fffffffLL) return VRVQ_ERR_ARG;
   // bf16x3 split path (conv_x3.h): stride-1 windows, a pre-split weight, the stage in LDS
-  a.mt_slow = conv_mt_slow();
   if constexpr (NW == 4 && BM <= 192 && (KS == 1 || KS == 2 || KS == 3 || KS == 7)) {
     constexpr int XW_MAX = (BN - 1) + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
-    if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX &&
-        x3_tile_ok(BM, BN, KS, a)) {
+    if (a.w3 != nullptr && a.stride == 1 && a.ssh == 0 && XW <= XW_MAX) {
       // pair tiles (conv_x3.h) need whole K-chunks: other Cin run the tile on plain chunks
       int rc = VRVQ_ERR_UNSUPPORTED;
       if (x3_pair<KS, BM, BN>() && a.cin % X3Cfg<KS, true>::CK == 0) {
@@ -549,21 +515,7 @@ int launch_cfg(const ConvArgs& a0, int batch, hipStream_t st) {
   return vrvq_launch_status();
 }
 
-static int conv_variant() {  // tuning override: VRVQ_CONV_VARIANT=0 (4-wave) | 1 (8-wave wide)
-  static const int v = [] {
-    const char* e = getenv("VRVQ_CONV_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 
-static int conv_bn_rule() {  // tuning override: VRVQ_CONV_BN_RULE=0 (minimise padding) | 1
-  static const int v = [] {  // (128 wide unless it pads more than 15 % of the columns)
-    const char* e = getenv("VRVQ_CONV_BN_RULE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 
 // Measured (profiles/r01j_conv_k1_ab.txt): 768 x 768 k1 + skip at T = 696, 485 -> 386 us with
 // 192-row tiles (384: 930 -> 922 us); 256-row tiles for 512 / 768 were slower (248 / 473 us).
@@ -702,8 +654,7 @@ int launch_splitk(const ConvArgs& a0, int batch, int S, hipStream_t st) {
     a.ks_split = S;
     a.n_mt = a.M / 128;
     a.n_nt = (a.ng + 95) / 96;
-    a.mt_slow = 0;
-    if (a.m_pad < a.n_mt * 128) return VRVQ_ERR_ARG;
+      if (a.m_pad < a.n_mt * 128) return VRVQ_ERR_ARG;
     const int XW = 95 + (KS - 1) * a.dil + 1;
     constexpr int XW_MAX = 95 + (KS - 1) * (KS == 7 ? 9 : 1) + 1;
     if (XW > XW_MAX) return VRVQ_ERR_UNSUPPORTED;
@@ -750,9 +701,8 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   // k = 16 (the stride-8 encoder convs): the 8 MB weight block does not fit in L2, so the
   // 128-wide tile's halved weight re-streaming beats its padding (1490 -> 1323 us at T = 696,
   // profiles/r02u_conv_ab.txt)
-  else if (a.ng < 4096 && KS != 16 && conv_bn_rule() == 0 && waste(64) * 10 < waste(128) * 7)
+  else if (a.ng < 4096 && KS != 16 && waste(64) * 10 < waste(128) * 7)
     bn = 64;
-  else if (a.ng < 4096 && conv_bn_rule() == 1 && waste(128) * 100 > a.ng * 15) bn = 64;
   else bn = 128;
   if (KS == 2 && bn == 64 && a.w3 != nullptr &&
       ((a.psh > 0 && conv_ph128() >= 1) || (a.up > 0 && conv_ph128() >= 2)))
@@ -774,16 +724,12 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   }
   if (bn == 32) return launch_cfg<128, 32, 4, 4, KS>(a, batch, st);
   if (bn == 96) return launch_cfg<128, 96, 4, 4, KS>(a, batch, st);
-  constexpr bool kWide = KS == 1 || KS == 2 || KS == 3 || KS == 7;  // register budget at 512 threads
-  const bool wide = kWide && conv_variant() == 1 && bn == 128 && a.ng >= 4096;
   if (a.M <= 64) {
     if (bn == 64) return launch_cfg<64, 64, 2, 4, KS>(a, batch, st);
-    if constexpr (kWide) if (wide) return launch_cfg<64, 256, 2, 8, KS>(a, batch, st);
     return launch_cfg<64, 128, 2, 4, KS>(a, batch, st);
   }
   // 96- and 192-row tiles: no padded rows for the C = 96 / 192 decoder blocks
   if (a.M <= 96) {
-    if constexpr (kWide) if (wide) return launch_cfg<96, 256, 1, 8, KS>(a, batch, st);
     return launch_cfg<96, 128, 1, 4, KS>(a, batch, st);
   }
   if (KS == 7 && conv_k7_192() && a.M % 192 == 0) {
@@ -807,7 +753,6 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
   }
   if ((KS >= 3 || (KS == 2 && a.up > 0)) && a.M % 128 != 0 && a.M % 192 == 0) {
     // (KS == 2 with up > 0: the polyphase ConvTranspose1d 192->96 s2, M = 192 phase rows)
-    if constexpr (kWide) if (wide) return launch_cfg<192, 256, 2, 8, KS>(a, batch, st);
     return launch_cfg<192, 128, 2, 4, KS>(a, batch, st);
   }
   if constexpr (KS == 1) {
@@ -825,7 +770,6 @@ int dispatch_tiles(const ConvArgs& a, int batch, hipStream_t st) {
     }
   }
   if (bn == 64) return launch_cfg<128, 64, 2, 4, KS>(a, batch, st);
-  if constexpr (kWide) if (wide) return launch_cfg<128, 256, 2, 8, KS>(a, batch, st);
   return launch_cfg<128, 128, 2, 4, KS>(a, batch, st);
 }
 

@@ -32,7 +32,6 @@ struct ConvArgs {
   int epi;
   int n_mt, n_nt;          // M tiles, N tiles
   const unsigned* w3;      // pre-split bf16 weight planes (conv_x3.h) or null: fp32 MFMA path
-  int mt_slow;             // block order: M tile slowest (all CUs on one weight tile: L2 reuse)
   // Strided conv (k = 2s, s = 2^psh) on the x3 loop as a stride-1 k = 2 conv over the
   // phase-split view xv[c*s + r][m] = x[c][m*s + r - ppad] (conv_x3.h): cin / tin above are the
   // view's (pcin * s, tout + 1), x is [B][pcin][ptin]. psh = 0: no view.
