@@ -1089,6 +1089,7 @@ struct FusedArgs {
                                     // bit 1 = chain parts skip the next stage's codebook
                                     // fragment loads (outputs wrong; timing only)
   int warm;                         // expansion workgroups pull the stage tables into L2 first
+  int poll2;                        // rvq_pt_kernel's loader keeps two looks in flight
 };
 
 // The stage tables the chain and the expansion read after stage 0 (normalised / raw codebooks,
@@ -1608,7 +1609,44 @@ __device__ __forceinline__ void pt_expand_body(const FusedArgs& f, int e, int N,
       if (si < 8) FSTAMP(f.stamps, 48 + si);  // the stage's stores issued (thread 0)
       cur = nxt;
     }
-    if (poll) {
+    if (poll && f.poll2) {
+      // two looks in flight: while one look's loads are checked the next one is already on its
+      // way, so a stage that lands just after a look is seen half a round trip later instead of
+      // a whole one (each sc1 look crosses to the chain part's XCD: ~1-2 us)
+      u32x4 h[PT_SL];
+      auto look_ok = [&](const u32x4 (&v)[PT_SL]) {
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u) ok = ok && v[u][1] == tag && v[u][3] == tag;
+        return __builtin_amdgcn_ballot_w64(!ok) == 0;
+      };
+      bool in_h = false;
+      for (unsigned it = 0;; ++it) {
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u)
+          h[u] = __builtin_amdgcn_raw_buffer_load_b128(zr, soff(u) + i * zstage, 0, CPOL_SC1);
+        if (look_ok(g)) break;
+        if (it >= f.spin_max) {
+          if (lane == 0) {
+            report_timeout(f.sync + SYNC_ERR, f.err_host, 2u);
+            xdead_s = 1;
+          }
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u)
+          g[u] = __builtin_amdgcn_raw_buffer_load_b128(zr, soff(u) + i * zstage, 0, CPOL_SC1);
+        if (look_ok(h)) {
+          in_h = true;
+          break;
+        }
+      }
+      if (in_h)
+#pragma unroll
+        for (int u = 0; u < PT_SL; ++u) g[u] = h[u];
+    } else if (poll) {  // one look in flight (VRVQ_RVQ_POLL2=0, the A/B)
       for (unsigned it = 0;; ++it) {
         bool ok = true;
 #pragma unroll
@@ -1627,6 +1665,8 @@ __device__ __forceinline__ void pt_expand_body(const FusedArgs& f, int e, int N,
         for (int u = 0; u < PT_SL; ++u)
           g[u] = __builtin_amdgcn_raw_buffer_load_b128(zr, soff(u) + i * zstage, 0, CPOL_SC1);
       }
+    }
+    if (poll) {
       if (i < 8) FSTAMPT(f.stamps, 56 + i, 64 * PT_LOADER);  // the stage's rows seen
       float* slab = sm + (i & 1) * PT_SLAB;
 #pragma unroll
@@ -2427,6 +2467,12 @@ extern "C" int vrvq_rvq_encode_part(const float* part, int batch, int dim, int f
     return e ? atoi(e) : 0;
   }();
   f.warm = warm;
+  // the loader's two looks in flight (VRVQ_RVQ_POLL2=0: one, the A/B)
+  static const int poll2 = [] {
+    const char* e = getenv("VRVQ_RVQ_POLL2");
+    return e ? atoi(e) : 1;
+  }();
+  f.poll2 = poll2;
   hipStream_t st = as_stream(stream);
   const size_t wsb = (size_t)workspace_bytes;
   switch (ncode / 256) {
