@@ -65,8 +65,9 @@ void conv_mfma_kernel(ConvArgs a) {
       // 64 NW threads x RM RN 16 floats, lane-contiguous: 256-B stores), no epilogue here
       constexpr int CK = X3Cfg<KS, PAIR>::CK;
       const int nch = (a.cin + CK - 1) / CK, per = (nch + a.ks_split - 1) / a.ks_split;
-      conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0, ks * per,
-                                                          min(nch, (ks + 1) * per));
+      if (ks * per < nch)  // (a forced part count can leave the last part empty: zero sums)
+        conv_mainloop_x3<BM, BN, WM, NW, KS, PH, PAIR, SB>(a, smem, acc, b, m0, n0, ks * per,
+                                                            min(nch, (ks + 1) * per));
       constexpr int NR = TC::RM * TC::RN * 16;
       const size_t tile = ((size_t)b * a.n_nt + nt) * a.n_mt + mt;
       const size_t ntile = (size_t)gridDim.x / a.ks_split;
